@@ -1,0 +1,469 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE.
+
+Run in the build container only (the reference is not on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+
+What is imported from /root/reference (read-only; nothing is copied):
+  * src.backgammon.get_all_possible_moves   (moves/generate_all_moves.py:7-66)
+  * src.backgammon.board.ImmutableBoard      (board/immutable_board.py:17-128)
+  * board/generate_board_tensor.compute_features (dead interleaved encoder, :98-140)
+  * environments/env_helper.py               (loaded by file path: execute_full_move_on_board_copy,
+                                              generate_all_board_features, reward predicates)
+  * agents/policy_network.py                 (loaded by file path: BackgammonPolicyNetwork)
+  * src/play/backgammon_256_standard_episode_2100000.pth (torch.load(weights_only=True))
+
+Two reference modules cannot be imported as-is because they need packages
+this image lacks (gym for environments/backgammon_env.py and, through
+src.environments, multi/two_ply.py). No stand-in modules are written for
+them. Instead the env-trajectory and 2-ply fixtures are produced by the
+helpers below, which call the reference's own functions in the order
+backgammon_env.py:92-221 and two_ply.py:93-150 do (restated orchestration,
+reference arithmetic); the docstrings cite the lines they follow.
+
+Inputs (board positions) come from seeded synthetic generators and from
+random-play trajectories driven by the CPU oracle (inputs only: every
+expected output below is computed by the reference).
+"""
+from __future__ import annotations
+
+import hashlib
+import importlib.util
+import os
+import sys
+import time
+
+sys.dont_write_bytecode = True
+import numpy as np
+import torch
+
+REF = os.environ.get("BGX_REFERENCE", "/root/reference")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path[:0] = [REF, os.path.join(REF, "src"), os.path.join(REPO, "oracle")]
+
+from src.backgammon import get_all_possible_moves  # noqa: E402
+from src.backgammon.board import ImmutableBoard  # noqa: E402
+from src.backgammon.board.generate_board_tensor import compute_features  # noqa: E402
+from src.backgammon.types import Player  # noqa: E402
+
+
+def _load(name, rel):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, rel))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+env_helper = _load("ref_env_helper", "src/environments/env_helper.py")
+policy_network = _load("ref_policy_network", "src/agents/policy_network.py")
+
+import oracle as orc  # noqa: E402  (inputs only)
+
+P1, P2 = Player.PLAYER1, Player.PLAYER2
+
+
+# ----------------------------------------------------------------- helpers
+def to_ib(b):
+    b = [int(x) for x in b]
+    return ImmutableBoard(positions_0=tuple(b[0:24]), positions_1=tuple(b[24:48]),
+                          bar=(b[48], b[49]), borne_off=(b[50], b[51]))
+
+
+def from_ib(ib):
+    return np.array(list(ib.positions_0) + list(ib.positions_1) + list(ib.bar)
+                    + list(ib.borne_off), np.uint8)
+
+
+def ref_moves(b, player, d0, d1):
+    ib = to_ib(b)
+    fms = get_all_possible_moves(Player(player), ib, [int(d0), int(d1)])
+    boards = [from_ib(env_helper.execute_full_move_on_board_copy(ib, fm)) for fm in fms]
+    nsub = [len(fm.sub_move_commands) for fm in fms]
+    subs = []
+    for fm in fms:
+        s = np.zeros((4, 3), np.uint8)
+        for j, sm in enumerate(fm.sub_move_commands):
+            s[j] = (int(sm.start), int(sm.end), int(bool(sm.hits_blot)))
+        subs.append(s)
+    return boards, nsub, subs
+
+
+def digest(boards):
+    h = hashlib.sha256()
+    for b in boards:
+        h.update(np.asarray(b, np.uint8).tobytes())
+    return np.frombuffer(h.digest(), np.uint8)
+
+
+INITIAL = from_ib(ImmutableBoard.initial_board())
+
+
+def rand_board(rng, mode):
+    """A valid board (15 checkers per player, no point held by both) and the
+    player to move. Modes: general, bar (checkers on the bar), bearoff (the
+    mover has everything home), race (both sides home: no contact)."""
+    b = np.zeros(52, np.uint8)
+    owner = np.full(24, -1)
+    mover = int(rng.integers(0, 2))
+    for pl in (0, 1):
+        home = list(range(18, 24)) if pl == 0 else list(range(0, 6))
+        if mode == "race" or (mode == "bearoff" and pl == mover):
+            region, bar = home, 0
+            off = int(rng.integers(0, 15))
+        else:
+            region = list(range(24))
+            bar = int(rng.integers(1, 4)) if (mode == "bar" or rng.random() < 0.15) else 0
+            off = int(rng.integers(0, 4)) if rng.random() < 0.2 else 0
+        rest = 15 - off - bar
+        b[48 + pl], b[50 + pl] = bar, off
+        while rest > 0:
+            cand = [i for i in region if owner[i] in (-1, pl)]
+            if not cand:
+                b[50 + pl] += rest
+                break
+            i = int(rng.choice(cand))
+            k = int(min(rest, rng.integers(1, 5) if rng.random() < 0.8 else rng.integers(1, 8)))
+            b[24 * pl + i] += k
+            owner[i] = pl
+            rest -= k
+    return b, mover
+
+
+def selfplay_positions(rng, n_games, max_steps=300):
+    """(board, player) along random-move games driven by the CPU oracle."""
+    out = []
+    for _ in range(n_games):
+        b = INITIAL.copy()
+        pl = int(rng.integers(0, 2))
+        for _s in range(max_steps):
+            d0, d1 = int(rng.integers(1, 7)), int(rng.integers(1, 7))
+            out.append((b.copy(), pl))
+            n, res, _ = orc.movegen(b, pl, d0, d1)
+            if n:
+                b = res[int(rng.integers(0, min(n, 500)))].copy()
+                if b[50 + pl] >= 15:
+                    break
+            pl = 1 - pl
+    return out
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    rng = np.random.default_rng(20260128)
+    t0 = time.time()
+
+    # ------------------------------------------------------------ positions
+    positions = []  # (board, player)
+    for pl in (0, 1):
+        positions.append((INITIAL.copy(), pl))
+    sp = selfplay_positions(rng, 60)
+    idx = rng.choice(len(sp), size=min(900, len(sp)), replace=False)
+    positions += [sp[i] for i in idx]
+    for mode, cnt in (("general", 250), ("bar", 150), ("bearoff", 250), ("race", 150)):
+        for _ in range(cnt):
+            positions.append(rand_board(rng, mode))
+    # survey §8c quirk: P1 on the bar, dice 3-5, pass-2 skip hides a 2-die play
+    q = np.zeros(52, np.uint8)
+    q[[4, 21, 22, 23]] = [1, 4, 6, 3]
+    q[24:24 + 13] = [2, 5, 0, 2, 0, 0, 1, 3, 0, 0, 0, 0, 2]
+    q[48] = 1
+    quirk = q
+    # game over boards (zero moves)
+    go = INITIAL.copy(); go[0:24] = 0; go[50] = 15
+    positions.append((go, 0))
+    # closed board + checker on bar (zero moves for some rolls)
+    cb = np.zeros(52, np.uint8)
+    cb[0:6] = 0; cb[24 + 0:24 + 6] = [2, 2, 2, 3, 3, 3]
+    cb[48] = 1; cb[0 + 12] = 14
+    positions.append((cb, 0))
+
+    # ------------------------------------------------------------ movegen cases
+    cases = []  # (board, player, d0, d1)
+    for pl in (0, 1):
+        for a in range(1, 7):
+            for c in range(a, 7):
+                cases.append((INITIAL, pl, c, a))  # sorted-desc and
+                if a != c:
+                    cases.append((INITIAL, pl, a, c))  # unsorted order
+    cases.append((quirk, 0, 3, 5))
+    cases.append((quirk, 0, 5, 3))
+    for d in range(1, 7):
+        for pl in (0, 1):
+            cases.append((cb, pl, d, d))
+            cases.append((go, 0, d, 7 - d if d != 7 - d else 1))
+    for b, pl in positions[:1600]:
+        d0, d1 = int(rng.integers(1, 7)), int(rng.integers(1, 7))
+        cases.append((b, pl, d0, d1))
+    # every roll on a subset (doubles-heavy coverage)
+    for b, pl in positions[2:60]:
+        for a in range(1, 7):
+            cases.append((b, pl, a, a))
+    # big doubles (>500 results) from spread-out boards
+    big = 0
+    tries = 0
+    while big < 12 and tries < 4000:
+        tries += 1
+        b = np.zeros(52, np.uint8)
+        pts = rng.choice(np.arange(0, 18), size=12, replace=False)
+        b[pts] = 1
+        b[pts[0]] += 3
+        b[24 + 18:24 + 24] = [3, 2, 3, 2, 3, 2]
+        d = int(rng.integers(1, 4))
+        n, _, _ = orc.movegen(b, 0, d, d)
+        if n > 500:
+            cases.append((b, 0, d, d))
+            big += 1
+    print(f"[gen] {len(cases)} explicit movegen cases ({big} >500-result doubles)", flush=True)
+
+    bo, pl_, dice, offs, rb, ns, sb = [], [], [], [0], [], [], []
+    for b, pl, d0, d1 in cases:
+        boards, nsub, subs = ref_moves(b, pl, d0, d1)
+        bo.append(np.asarray(b, np.uint8)); pl_.append(pl); dice.append((d0, d1))
+        rb += boards; ns += nsub; sb += subs
+        offs.append(offs[-1] + len(boards))
+    np.savez_compressed(
+        os.path.join(OUT, "movegen_cases.npz"), boards=np.stack(bo), player=np.array(pl_, np.uint8),
+        dice=np.array(dice, np.uint8), offsets=np.array(offs, np.int64),
+        results=np.stack(rb) if rb else np.zeros((0, 52), np.uint8),
+        nsub=np.array(ns, np.uint8), subs=np.stack(sb) if sb else np.zeros((0, 4, 3), np.uint8))
+    print(f"[gen] movegen_cases: {len(cases)} cases, {len(rb)} result boards "
+          f"({time.time() - t0:.1f}s)", flush=True)
+
+    # ------------------------------------------------------------ movegen digests
+    dg_b, dg_p, dg_d, dg_n, dg_h = [], [], [], [], []
+    sp2 = selfplay_positions(rng, 150)
+    pick = rng.choice(len(sp2), size=min(9000, len(sp2)), replace=False)
+    pool = [sp2[i] for i in pick]
+    for mode, cnt in (("general", 1500), ("bar", 800), ("bearoff", 1500), ("race", 700)):
+        pool += [rand_board(rng, mode) for _ in range(cnt)]
+    for b, pl in pool:
+        d0, d1 = int(rng.integers(1, 7)), int(rng.integers(1, 7))
+        boards, _, _ = ref_moves(b, pl, d0, d1)
+        dg_b.append(b); dg_p.append(pl); dg_d.append((d0, d1)); dg_n.append(len(boards))
+        dg_h.append(digest(boards))
+    np.savez_compressed(os.path.join(OUT, "movegen_digests.npz"), boards=np.stack(dg_b),
+                        player=np.array(dg_p, np.uint8), dice=np.array(dg_d, np.uint8),
+                        count=np.array(dg_n, np.int32), sha256=np.stack(dg_h))
+    print(f"[gen] movegen_digests: {len(pool)} cases ({time.time() - t0:.1f}s)", flush=True)
+
+    # ------------------------------------------------------------ encodings
+    enc_b = np.concatenate([np.stack([b for b, _ in positions]), np.stack(rb[:1500])])
+    enc_p = np.concatenate([np.array([p for _, p in positions]),
+                            rng.integers(0, 2, size=min(1500, len(rb)))]).astype(np.uint8)
+    live = np.stack([to_ib(b).get_board_features(Player(int(p))).numpy()
+                     for b, p in zip(enc_b, enc_p)])
+    inter = []
+    for b, p in zip(enc_b[:600], enc_p[:600]):
+        b8 = b.astype(np.int8)
+        inter.append(compute_features(b8[0:24], b8[24:48], b8[48:50], b8[50:52],
+                                      Player(int(p))).numpy())
+    np.savez_compressed(os.path.join(OUT, "encode.npz"), boards=enc_b, player=enc_p,
+                        live=live.astype(np.float32), interleaved=np.stack(inter).astype(np.float32))
+    print(f"[gen] encode: {len(enc_b)} boards ({time.time() - t0:.1f}s)", flush=True)
+
+    # ------------------------------------------------------------ weights + V
+    torch.manual_seed(0)
+    net0 = policy_network.BackgammonPolicyNetwork()
+    sd = torch.load(os.path.join(REF, "src/play/backgammon_256_standard_episode_2100000.pth"),
+                    map_location="cpu", weights_only=True)
+    netc = policy_network.BackgammonPolicyNetwork()
+    netc.load_state_dict(sd)
+
+    def wdict(net):
+        s = net.state_dict()
+        return dict(W1=s["fc1.weight"].numpy().astype(np.float32),
+                    b1=s["fc1.bias"].numpy().astype(np.float32),
+                    w2=s["value_head.weight"].numpy().reshape(-1).astype(np.float32),
+                    b2=s["value_head.bias"].numpy().reshape(-1).astype(np.float32))
+
+    w0, wc = wdict(net0), wdict(netc)
+    np.savez(os.path.join(OUT, "weights_seed0.npz"), **w0)
+    np.savez(os.path.join(OUT, "weights_ckpt2100000.npz"), **wc)
+    with torch.no_grad():
+        X = torch.from_numpy(live)
+        v0 = net0(X).numpy()
+        vc = netc(X).numpy()
+    np.savez_compressed(os.path.join(OUT, "value.npz"), x=live.astype(np.float32), v_seed0=v0,
+                        v_ckpt=vc)
+    print(f"[gen] value: {len(live)} rows ({time.time() - t0:.1f}s)", flush=True)
+
+    # ------------------------------------------------------------ predicates
+    pr_b = enc_b
+    preds = {k: [] for k in ("game_over", "gammon", "backgammon", "prime", "closed_out")}
+    pr_p = []
+    for b in pr_b:
+        ib = to_ib(b)
+        for p in (P1, P2):
+            pr_p.append(int(p))
+            preds["game_over"].append(env_helper.check_game_over(ib, p))
+            preds["gammon"].append(env_helper.check_for_gammon(ib, p))
+            preds["backgammon"].append(env_helper.check_for_backgammon(ib, p))
+            preds["prime"].append(env_helper.made_at_least_five_prime(ib, p))
+            preds["closed_out"].append(env_helper.is_closed_out(ib, p))
+    np.savez_compressed(os.path.join(OUT, "predicates.npz"), boards=np.repeat(pr_b, 2, axis=0),
+                        player=np.array(pr_p, np.uint8),
+                        **{k: np.array(v, bool) for k, v in preds.items()})
+    print(f"[gen] predicates ({time.time() - t0:.1f}s)", flush=True)
+
+    # ------------------------------------------------------------ env trajectories
+    gen_env_trajectories(net0, rng, t0)
+
+    # ------------------------------------------------------------ 2-ply
+    gen_two_ply(net0, netc, positions, rng, t0)
+    print(f"[gen] done in {time.time() - t0:.1f}s")
+
+
+REWARD_WIN = {"backgammon": 2.5, "gammon": 2.0, "regular": 1.0}
+WIN_CODE = {None: 0, "regular": 1, "gammon": 2, "backgammon": 3}
+
+
+def greedy_episode(net, dice_rng, max_steps=300, max_legal=500):
+    """One greedy (argmax V) episode with recorded dice. Orchestration follows
+    BackgammonEnv.reset/step (backgammon_env.py:92-128, 130-221, 223-308) and
+    Worker.play_episode (worker.py:78-174) with argmax in place of sampling
+    (play_versus_ai.py:188-195); every rule is the reference's function."""
+    dice = []
+
+    def roll():
+        r = [int(dice_rng.integers(1, 7)), int(dice_rng.integers(1, 7))]
+        dice.extend(r)
+        return r
+
+    def legal(board, player, r):
+        fms = get_all_possible_moves(player, board, r)
+        full = len(fms)
+        fms = fms[:max_legal]
+        return fms, full
+
+    board = ImmutableBoard.initial_board()
+    r = roll()
+    while r[0] == r[1]:
+        r = roll()
+    player = P2 if r[0] < r[1] else P1
+    r = roll()
+    while r[0] == r[1]:
+        r = roll()
+    fms, full = legal(board, player, r)
+    close_given = {P1: False, P2: False}
+    prime_given = {P1: False, P2: False}
+    rec = []
+    done = False
+    step = 0
+    while not done and step < max_steps:
+        row = dict(board=from_ib(board), player=int(player), roll=tuple(r), num_moves=len(fms),
+                   full_moves=full, action=-1, reward=0.0, done=False, win_type=0, close_out=False,
+                   prime=False, kind=1)
+        if not fms:
+            player = P2 if player == P1 else P1
+            r = roll()
+            fms, full = legal(board, player, r)
+            rec.append(row)
+            step += 1
+            continue
+        feats = env_helper.generate_all_board_features(board, player, fms)
+        obs = board.get_board_features(player)
+        with torch.no_grad():
+            v = net(torch.cat([obs.unsqueeze(0), feats], 0))
+        a = int(torch.argmax(v[1:]).item())
+        row.update(action=a, kind=0, v_obs=float(v[0]), v_act=float(v[1 + a]))
+        board = env_helper.execute_full_move_on_board_copy(board, fms[a])
+        reward = torch.tensor(0.0)
+        if env_helper.check_game_over(board, player):
+            if env_helper.check_for_backgammon(board, player):
+                wt = "backgammon"
+            elif env_helper.check_for_gammon(board, player):
+                wt = "gammon"
+            else:
+                wt = "regular"
+            reward = torch.tensor(REWARD_WIN[wt])
+            row.update(win_type=WIN_CODE[wt], done=True)
+            done = True
+        else:
+            if env_helper.is_closed_out(board, player) and not close_given[player]:
+                reward += torch.tensor(0.30)
+                close_given[player] = True
+                row["close_out"] = True
+            if env_helper.made_at_least_five_prime(board, player) and not prime_given[player]:
+                reward += torch.tensor(0.20)
+                prime_given[player] = True
+                row["prime"] = True
+            player = P2 if player == P1 else P1
+            r = roll()
+            fms, full = legal(board, player, r)
+        row["reward"] = float(reward.item())
+        row["after"] = from_ib(board)
+        rec.append(row)
+        step += 1
+    return dice, rec
+
+
+def gen_env_trajectories(net, rng, t0):
+    dice_rng = np.random.default_rng(7)
+    D, S = [], []
+    ep = []
+    for e in range(16):
+        dice, rec = greedy_episode(net, dice_rng)
+        ep.append((len(D), len(dice), len(S), len(rec)))
+        D += dice
+        S += rec
+    keys = ["player", "num_moves", "full_moves", "action", "reward", "done", "win_type",
+            "close_out", "prime", "kind"]
+    arrs = {k: np.array([s[k] for s in S]) for k in keys}
+    arrs["board"] = np.stack([s["board"] for s in S])
+    arrs["after"] = np.stack([s.get("after", s["board"]) for s in S])
+    arrs["roll"] = np.array([s["roll"] for s in S], np.uint8)
+    arrs["v_obs"] = np.array([s.get("v_obs", 0.0) for s in S], np.float32)
+    arrs["v_act"] = np.array([s.get("v_act", 0.0) for s in S], np.float32)
+    arrs["reward"] = arrs["reward"].astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "env_traj.npz"), dice=np.array(D, np.int32),
+                        episodes=np.array(ep, np.int64), **arrs)
+    print(f"[gen] env_traj: {len(ep)} episodes, {len(S)} steps ({time.time() - t0:.1f}s)",
+          flush=True)
+
+
+DICE_ROLLS = [[1, 1], [1, 2], [1, 3], [1, 4], [1, 5], [1, 6], [2, 2], [2, 3], [2, 4], [2, 5],
+              [2, 6], [3, 3], [3, 4], [3, 5], [3, 6], [4, 4], [4, 5], [4, 6], [5, 5], [5, 6],
+              [6, 6]]
+COUNTS = [1, 2, 2, 2, 2, 2, 1, 2, 2, 2, 2, 1, 2, 2, 2, 1, 2, 2, 1, 2, 1]
+
+
+def weighted_opponent_response(board, opponent, net):
+    """compute_weighted_opponent_response (two_ply.py:93-150), exact mode:
+    the random.sample subsampling for 1-1/2-2/3-3 (two_ply.py:119-121) is
+    skipped."""
+    total = 0.0
+    for roll, cnt in zip(DICE_ROLLS, COUNTS):
+        moves = get_all_possible_moves(opponent, board, roll)
+        if moves:
+            feats = env_helper.generate_all_board_features(board, opponent, moves)
+            with torch.no_grad():
+                sv = net.forward(feats).view(-1)
+            top = torch.sort(sv, descending=True)[0][:5]
+            total += top.mean().item() * (cnt / 36)
+    return total
+
+
+def gen_two_ply(net0, netc, positions, rng, t0):
+    pick = rng.choice(np.arange(2, len(positions)), size=60, replace=False)
+    B, O, W0, WC = [], [], [], []
+    for i in pick:
+        b, pl = positions[int(i)]
+        # the board after the mover's move: the first result of a random roll
+        d0, d1 = int(rng.integers(1, 7)), int(rng.integers(1, 7))
+        boards, _, _ = ref_moves(b, pl, d0, d1)
+        after = boards[0] if boards else b
+        ib = to_ib(after)
+        opp = P2 if pl == 0 else P1
+        B.append(after); O.append(int(opp))
+        W0.append(weighted_opponent_response(ib, opp, net0))
+        WC.append(weighted_opponent_response(ib, opp, netc))
+    np.savez_compressed(os.path.join(OUT, "two_ply.npz"), boards=np.stack(B),
+                        opponent=np.array(O, np.uint8), w_seed0=np.array(W0),
+                        w_ckpt=np.array(WC))
+    print(f"[gen] two_ply: {len(B)} positions ({time.time() - t0:.1f}s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
