@@ -1,0 +1,154 @@
+/*
+ * bgx.h — C-ABI of libbgx.so, the MI355X (gfx950) self-play engine for the
+ * backgammon TD learner of Nick-qsv/MLP-PPO-2PLY-MULTI.
+ *
+ * The reference has no native boundary; its hot path is Python called in
+ * process by the rollout worker. Each entry point below states the reference
+ * interface it replaces (file:line under the reference's src/). A Python
+ * ctypes binding that mirrors the reference's src/multi surface is shipped in
+ * mlp-ppo-2ply-multi_amd/bgx; INTEGRATION.md shows the stub a maintainer adds.
+ *
+ * Conventions
+ *  - Every call returns int: 0 = ok, < 0 = error (BGX_E_*); the message of
+ *    the last error on the calling thread is bgx_last_error(). No exceptions,
+ *    aborts or printing cross the ABI.
+ *  - Pointers named d_* are DEVICE pointers (e.g. torch .data_ptr() of a
+ *    cuda tensor) and calls taking `stream` (a hipStream_t, NULL = default)
+ *    are asynchronous on it. Pointers named h_* are host pointers.
+ *  - Boards are the reference's ImmutableBoard fields as u8[52]:
+ *    positions_0[24] | positions_1[24] | bar[2] | borne_off[2]
+ *    (board/immutable_board.py:16-24); player 0 = PLAYER1, 1 = PLAYER2
+ *    (types/moves.py:36-42).
+ */
+#ifndef BGX_H
+#define BGX_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BGX_ABI_VERSION 1
+
+#define BGX_OK 0
+#define BGX_E_ARG -1        /* invalid argument */
+#define BGX_E_HIP -2        /* HIP runtime error */
+#define BGX_E_CAPACITY -3   /* a device buffer overflowed (see message) */
+#define BGX_E_STATE -4      /* call not valid in the current state */
+
+int bgx_abi_version(void);
+const char* bgx_last_error(void);
+
+/* ---------------- stateless parity entry points ---------------- */
+
+/* get_all_possible_moves (backgammon/moves/generate_all_moves.py:7-90) for n
+ * (board, player, dice) jobs, followed by execute_full_move_on_board_copy of
+ * every FullMove (environments/env_helper.py:27-91): d_out_boards[j][k] (u8[52])
+ * is the k-th result board of job j in the reference's order, for k < cap;
+ * d_out_count[j] is the full number of results (may exceed cap). */
+int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t* d_dice, int n,
+                uint8_t* d_out_boards, int32_t* d_out_count, int cap, void* stream);
+
+/* ImmutableBoard.get_board_features (board/immutable_board.py:86-128) for
+ * layout 0, generate_board_tensor.compute_features (:98-140) for layout 1;
+ * d_out is float32 [n][198]. */
+int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d_out, int layout,
+               void* stream);
+
+/* ---------------- value network ---------------- */
+typedef struct bgx_net bgx_net;
+
+/* BackgammonPolicyNetwork (agents/policy_network.py:36-70) weights, host fp32:
+ * h_W1 [128][198] (fc1.weight), h_b1 [128], h_w2 [128] (value_head.weight), h_b2 [1]. */
+int bgx_net_create(const float* h_W1, const float* h_b1, const float* h_w2, const float* h_b2,
+                   bgx_net** out);
+int bgx_net_destroy(bgx_net* net);
+/* forward (policy_network.py:53-70) on arbitrary fp32 features d_x [n][198] -> d_out [n] */
+int bgx_value(const bgx_net* net, const float* d_x, int n, float* d_out, void* stream);
+/* fused encode + forward on boards (the engine's MFMA path): V of
+ * get_board_features(board, player) for n boards -> d_out [n] */
+int bgx_value_boards(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_player, int n,
+                     float* d_out, void* stream);
+
+/* ---------------- self-play engine ---------------- */
+typedef struct bgx_engine bgx_engine;
+
+typedef struct bgx_config {
+    int lanes;              /* game lanes on this device */
+    int lane_base;          /* global id of lane 0 (RNG streams keyed by global lane id) */
+    uint64_t seed;
+    int ply;                /* 1 = worker.py:78-174 softmax(V/T); 2 = two_ply.py scoring */
+    int k_top;              /* 2-ply candidates: 4 (reference, two_ply.py:67-70) or 0 = all */
+    float alpha, beta;      /* 2-ply score = alpha*S - beta*W (two_ply.py:44-50): 1.0, 0.9 */
+    int max_steps;          /* MAX_TIMESTEPS (config/configuration.py:4): 300 */
+    int max_legal;          /* BackgammonEnv max_legal_moves (backgammon_env.py:35): 500 */
+    int ring;               /* experience ring slots per lane (>= max_steps + steps between harvests) */
+    int ep_cap;             /* finished-episode headers held between harvests */
+    int cand_per_lane;      /* average candidate rows reserved per lane (1-ply buffer) */
+    int reply_per_lane;     /* average 2-ply reply rows reserved per lane */
+} bgx_config;
+
+void bgx_config_default(bgx_config* cfg);
+
+/* Replaces the per-process Worker (multi/worker.py:17-45) + BackgammonEnv
+ * (environments/backgammon_env.py:29-128): `lanes` independent games on one
+ * device, all reset per BackgammonEnv.reset. */
+int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out);
+int bgx_engine_destroy(bgx_engine* e);
+
+/* ParameterManager.get_parameters / get_temperature hand-off
+ * (multi/parameter_manager.py:54-111, worker.py:66-76): host fp32 weights as
+ * in bgx_net_create, the sampling temperature and the parameter version. */
+int bgx_set_weights(bgx_engine* e, const float* h_W1, const float* h_b1, const float* h_w2,
+                    const float* h_b2, float temperature, uint64_t version);
+
+/* Advance every lane by n_steps env steps (one BackgammonEnv.step each,
+ * passes included; finished games are recorded and the lane restarts). */
+int bgx_step(bgx_engine* e, int n_steps, void* stream);
+/* Wait for the engine's stream; reports device-side overflow flags. */
+int bgx_sync(bgx_engine* e);
+
+/* Finished episodes since the last harvest (Episode/Experience,
+ * environments/episode.py:5-84). Both arrays are DEVICE memory owned by the
+ * engine, valid until the next bgx_harvest/bgx_step:
+ *   headers [n_episodes][8] u32: global lane, episode no., first record,
+ *     n_records, env steps, win_type | winner << 8 | flags << 16
+ *   records [n_records][24] u32: before board (packed, 8 u32), after board
+ *     (packed), V(s) f32, V(a) f32, reward f32, action | n_moves << 16,
+ *     dice0 | dice1 << 8 | done << 16 | close_out << 17 | prime << 18 |
+ *     mover << 19 | win_type << 20, episode no., step, global lane.
+ * Packed board: u32[8]: P1 point nibbles [0..2], P2 [3..5], w[6] = bar1 |
+ * bar2 << 4 | off1 << 8 | off2 << 12 | indicator player << 16.
+ * Synchronizes the engine stream. */
+typedef struct bgx_harvest_info {
+    int n_episodes;
+    int n_records;
+    const uint32_t* d_headers;
+    const uint32_t* d_records;
+} bgx_harvest_info;
+int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream);
+
+typedef struct bgx_stats {
+    uint64_t env_steps;     /* lane steps (passes included) */
+    uint64_t decisions;     /* non-pass steps (one Experience each) */
+    uint64_t episodes;
+    uint64_t value_rows;    /* boards evaluated by the value MLP */
+    uint64_t movegen_jobs;  /* (board, dice) move generations */
+    uint64_t fallback_jobs; /* doubles jobs re-run on the global-memory path */
+} bgx_stats;
+int bgx_get_stats(bgx_engine* e, bgx_stats* out);  /* synchronizes */
+
+/* Kernel timing (HIP events on the engine stream, recorded per bgx_step while
+ * enabled): total milliseconds and launch counts of the movegen and MLP
+ * kernels since the last reset. */
+int bgx_set_timing(bgx_engine* e, int enabled);
+int bgx_get_timing(bgx_engine* e, double* ms_movegen, int* n_movegen, double* ms_mlp, int* n_mlp);
+
+/* Convert between u8[52] boards and the engine's packed boards (device). */
+int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream);
+int bgx_unpack(const uint32_t* d_packed, int n, uint8_t* d_boards, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,74 @@
+"""Harvested compact records -> the reference's Episode / Experience objects.
+
+Experience fields after Episode.to_numpy() (src/environments/episode.py:5-46,
+src/multi/worker.py:149-168): observation / next_observation np.float32[198]
+(features of the board with the indicator of the player to move, or of the
+winner at a terminal step), state_value / next_state_value Python floats,
+reward np.float32 0-d array, done bool. Episode carries win_type and
+close_out_counts / prime_reward_counts keyed by the players who made a
+decision (episode.py:56-76). Observations are re-encoded on the GPU from the
+packed boards (bgx_encode), not stored as 198 floats per step.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+from .engine import WIN_TYPES, Harvest
+
+
+def decode_records(records: torch.Tensor):
+    """records int32 [m, 24] (device) -> dict of host numpy arrays, with the
+    198-d observations encoded on the device."""
+    m = records.shape[0]
+    if m == 0:
+        z = np.zeros((0, 198), np.float32)
+        return dict(obs=z, next_obs=z, v_s=np.zeros(0, np.float32), v_a=np.zeros(0, np.float32),
+                    reward=np.zeros(0, np.float32), done=np.zeros(0, bool), action=np.zeros(0, np.int32),
+                    n_moves=np.zeros(0, np.int32), dice=np.zeros((0, 2), np.int32),
+                    close_out=np.zeros(0, bool), prime=np.zeros(0, bool), mover=np.zeros(0, np.int32),
+                    win_type=np.zeros(0, np.int32), before=np.zeros((0, 52), np.uint8),
+                    after=np.zeros((0, 52), np.uint8), step=np.zeros(0, np.int32))
+    before, after = records[:, 0:8].contiguous(), records[:, 8:16].contiguous()
+    b8, a8 = ops.unpack(before), ops.unpack(after)
+    obs = ops.encode(b8, ops.packed_player(before))
+    nxt = ops.encode(a8, ops.packed_player(after))
+    tail = records[:, 16:24].cpu().numpy()
+    f = tail[:, 0:3].copy().view(np.float32)
+    w3, w4 = tail[:, 3].astype(np.uint32), tail[:, 4].astype(np.uint32)
+    return dict(
+        obs=obs.cpu().numpy(), next_obs=nxt.cpu().numpy(), v_s=f[:, 0], v_a=f[:, 1], reward=f[:, 2],
+        action=(w3 & 0xFFFF).astype(np.int32), n_moves=(w3 >> 16).astype(np.int32),
+        dice=np.stack([(w4 & 0xFF), (w4 >> 8) & 0xFF], 1).astype(np.int32),
+        done=((w4 >> 16) & 1).astype(bool), close_out=((w4 >> 17) & 1).astype(bool),
+        prime=((w4 >> 18) & 1).astype(bool), mover=((w4 >> 19) & 1).astype(np.int32),
+        win_type=((w4 >> 20) & 7).astype(np.int32), before=b8.cpu().numpy(), after=a8.cpu().numpy(),
+        step=tail[:, 6].astype(np.int32))
+
+
+def to_episodes(h: Harvest, episode_cls, experience_cls, player_enum):
+    """Build reference-shaped Episode objects (already in to_numpy() form)."""
+    hdr = h.headers.cpu().numpy().astype(np.uint32)
+    d = decode_records(h.records)
+    eps = []
+    o = 0
+    for row in hdr:
+        n = int(row[3])
+        ep = episode_cls()
+        for k in range(o, o + n):
+            ex = experience_cls(observation=d["obs"][k], state_value=float(d["v_s"][k]),
+                                reward=np.array(d["reward"][k], dtype=np.float32), done=bool(d["done"][k]),
+                                next_observation=d["next_obs"][k], next_state_value=float(d["v_a"][k]))
+            info = {"current_player": player_enum(int(d["mover"][k]))}
+            if d["win_type"][k]:
+                info["win_type"] = WIN_TYPES[int(d["win_type"][k])]
+                info["winner"] = player_enum(int(d["mover"][k]))
+            if d["close_out"][k]:
+                info["close_out_reward"] = True
+            if d["prime"][k]:
+                info["prime_reward"] = True
+            ep.add_experience(ex, info)
+        o += n
+        eps.append(ep)
+    return eps

@@ -1,0 +1,139 @@
+"""Stateless device ops over libbgx.so (the parity entry points of include/bgx.h).
+
+Each op mirrors one reference function on a batch of boards:
+  movegen      get_all_possible_moves + execute_full_move_on_board_copy
+               (backgammon/moves/generate_all_moves.py:7-90, environments/env_helper.py:27-91)
+  encode       ImmutableBoard.get_board_features (board/immutable_board.py:86-128),
+               layout=1: generate_board_tensor.compute_features (:98-140)
+  Net.value    BackgammonPolicyNetwork.forward (agents/policy_network.py:53-70)
+Boards are uint8 [n, 52] device tensors in the reference's field order.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import check, lib, ptr, require_cuda, stream_handle
+
+
+def _u8(t, shape_last=None):
+    t = torch.as_tensor(t)
+    if t.dtype != torch.uint8:
+        t = t.to(torch.uint8)
+    if not t.is_cuda:
+        t = t.cuda()
+    return t.contiguous()
+
+
+def movegen(boards, player, dice, cap: int = 512, stream=None):
+    """Ordered result boards for n (board, player, dice) jobs.
+
+    Returns (out uint8 [n, cap, 52], count int32 [n]); count is the full
+    number of results, rows k >= min(count, cap) are unspecified."""
+    boards, player, dice = _u8(boards).view(-1, 52), _u8(player).view(-1), _u8(dice).view(-1, 2)
+    n = boards.shape[0]
+    require_cuda(boards, player, dice)
+    out = torch.empty((n, cap, 52), dtype=torch.uint8, device=boards.device)
+    cnt = torch.empty((n,), dtype=torch.int32, device=boards.device)
+    check(lib().bgx_movegen(ptr(boards), ptr(player), ptr(dice), n, ptr(out), ptr(cnt), cap,
+                            stream_handle(stream)), "bgx_movegen")
+    return out, cnt
+
+
+def encode(boards, player, layout: int = 0, stream=None):
+    boards, player = _u8(boards).view(-1, 52), _u8(player).view(-1)
+    require_cuda(boards, player)
+    n = boards.shape[0]
+    out = torch.empty((n, 198), dtype=torch.float32, device=boards.device)
+    check(lib().bgx_encode(ptr(boards), ptr(player), n, ptr(out), int(layout), stream_handle(stream)),
+          "bgx_encode")
+    return out
+
+
+def pack(boards, player, stream=None):
+    boards, player = _u8(boards).view(-1, 52), _u8(player).view(-1)
+    require_cuda(boards, player)
+    n = boards.shape[0]
+    out = torch.empty((n, 8), dtype=torch.int32, device=boards.device)
+    check(lib().bgx_pack(ptr(boards), ptr(player), n, ptr(out), stream_handle(stream)), "bgx_pack")
+    return out
+
+
+def unpack(packed, stream=None):
+    """Packed boards (int32 [n, 8]) -> uint8 [n, 52]; the indicator player is
+    bits 16.. of word 6."""
+    packed = torch.as_tensor(packed).contiguous()
+    require_cuda(packed)
+    n = packed.shape[0]
+    out = torch.empty((n, 52), dtype=torch.uint8, device=packed.device)
+    check(lib().bgx_unpack(ptr(packed), n, ptr(out), stream_handle(stream)), "bgx_unpack")
+    return out
+
+
+def packed_player(packed):
+    return ((packed[:, 6] >> 16) & 1).to(torch.uint8)
+
+
+def weights_from(obj):
+    """Host fp32 (W1 [128,198], b1 [128], w2 [128], b2 [1]) from a state_dict
+    (fc1.weight, fc1.bias, value_head.weight, value_head.bias) or a dict with
+    keys W1, b1, w2, b2."""
+    if "fc1.weight" in obj:
+        W1, b1 = obj["fc1.weight"], obj["fc1.bias"]
+        w2, b2 = obj["value_head.weight"], obj["value_head.bias"]
+    else:
+        W1, b1, w2, b2 = obj["W1"], obj["b1"], obj["w2"], obj["b2"]
+
+    def f(x, shape):
+        if isinstance(x, torch.Tensor):
+            x = x.detach().float().cpu().numpy()
+        return np.ascontiguousarray(np.asarray(x, dtype=np.float32).reshape(shape))
+
+    W1 = f(W1, (128, 198))
+    if W1.shape != (128, 198):
+        raise ValueError("fc1.weight must be [128, 198] (BackgammonPolicyNetwork hidden_size=128)")
+    return W1, f(b1, (128,)), f(w2, (128,)), f(b2, (1,))
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Net:
+    """Device copy of BackgammonPolicyNetwork weights (fp32 + split-fp16 MFMA fragments)."""
+
+    def __init__(self, weights):
+        W1, b1, w2, b2 = weights_from(weights)
+        if not torch.cuda.is_available():
+            require_cuda()
+        h = ctypes.c_void_p()
+        check(lib().bgx_net_create(_fp(W1), _fp(b1), _fp(w2), _fp(b2), ctypes.byref(h)),
+              "bgx_net_create")
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value:
+            lib().bgx_net_destroy(h)
+            self._h = None
+
+    def value(self, x, stream=None):
+        """V for fp32 features [n, 198] (generic fp32 FMA path)."""
+        x = torch.as_tensor(x, dtype=torch.float32)
+        if not x.is_cuda:
+            x = x.cuda()
+        x = x.contiguous().view(-1, 198)
+        out = torch.empty((x.shape[0],), dtype=torch.float32, device=x.device)
+        check(lib().bgx_value(self._h, ptr(x), x.shape[0], ptr(out), stream_handle(stream)), "bgx_value")
+        return out
+
+    def value_boards(self, boards, player, stream=None):
+        """V of get_board_features(board, player) via the fused split-fp16 MFMA kernel."""
+        boards, player = _u8(boards).view(-1, 52), _u8(player).view(-1)
+        require_cuda(boards, player)
+        out = torch.empty((boards.shape[0],), dtype=torch.float32, device=boards.device)
+        check(lib().bgx_value_boards(self._h, ptr(boards), ptr(player), boards.shape[0], ptr(out),
+                                     stream_handle(stream)), "bgx_value_boards")
+        return out

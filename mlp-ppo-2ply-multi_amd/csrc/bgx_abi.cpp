@@ -1,0 +1,648 @@
+// bgx_abi.cpp — the extern "C" boundary of libbgx.so (declared in include/bgx.h).
+//
+// Host-side orchestration only: argument checks, device buffers, the
+// per-step launch sequence and error reporting. All game logic runs in the
+// HIP kernels (bgx_movegen.hip, bgx_mlp.hip, bgx_encode.hip, bgx_engine.hip).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bgx.h"
+#include "bgx_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(BGX_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));       \
+    } while (0)
+
+constexpr int KSTEPS = 13;
+constexpr int NFRAG = 2 * 4 * KSTEPS * 64;
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T) + 16);
+    if (e != hipSuccess) return fail(BGX_E_HIP, "hipMalloc(%zu B): %s", n * sizeof(T), hipGetErrorString(e));
+    return BGX_OK;
+}
+
+}  // namespace
+
+struct bgx_net {
+    float* W1 = nullptr;   // fp32 copies (bgx_value)
+    float* b1 = nullptr;
+    float* w2 = nullptr;
+    float b2 = 0.0f;
+    uint4* wfrag = nullptr;   // split-fp16 MFMA fragments
+    float* rowc = nullptr;    // [128][4]: 2^-e, w2, b1, 0
+    uint32_t* scratch = nullptr;   // packed boards for bgx_value_boards
+    int scratch_n = 0;
+};
+
+// Split-fp16 fragments (see bgx_mlp.hip header for the scheme).
+static void build_fragments(const float* W1, const float* b1, const float* w2,
+                            std::vector<uint16_t>& frag, std::vector<float>& rowc) {
+    std::vector<double> Wp(128 * 198);
+    for (int j = 0; j < 128; ++j)
+        for (int k = 0; k < 198; ++k) {
+            double v = W1[j * 198 + k];
+            if (k == 193 || k == 195) v /= 15.0;   // feature = integer borne-off count
+            Wp[j * 198 + k] = v;
+        }
+    std::vector<_Float16> hi(128 * 208), lo(128 * 208);
+    rowc.assign(128 * 4, 0.0f);
+    for (int j = 0; j < 128; ++j) {
+        double mx = 0.0;
+        for (int k = 0; k < 198; ++k) mx = std::fmax(mx, std::fabs(Wp[j * 198 + k]));
+        int e = 0;
+        if (mx > 0.0) {
+            e = 14 - (int)std::floor(std::log2(mx));
+            if (e > 100) e = 100;
+            if (e < -100) e = -100;
+        }
+        const double sc = std::ldexp(1.0, e);
+        for (int k = 0; k < 208; ++k) {
+            const double x = k < 198 ? Wp[j * 198 + k] * sc : 0.0;
+            const _Float16 h = (_Float16)(float)x;
+            hi[j * 208 + k] = h;
+            lo[j * 208 + k] = (_Float16)(float)(x - (double)(float)h);
+        }
+        rowc[j * 4 + 0] = (float)std::ldexp(1.0, -e);
+        rowc[j * 4 + 1] = w2[j];
+        rowc[j * 4 + 2] = b1[j];
+    }
+    frag.assign((size_t)NFRAG * 8, 0);
+    for (int t = 0; t < 2; ++t)
+        for (int m = 0; m < 4; ++m)
+            for (int s = 0; s < KSTEPS; ++s)
+                for (int l = 0; l < 64; ++l)
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const int row = 32 * m + (l & 31);
+                        const int k = 16 * s + 8 * (l >> 5) + jj;
+                        const _Float16 v = (t == 0 ? hi : lo)[row * 208 + k];
+                        uint16_t bits;
+                        std::memcpy(&bits, &v, 2);
+                        frag[((((size_t)t * 4 + m) * KSTEPS + s) * 64 + l) * 8 + jj] = bits;
+                    }
+}
+
+static int net_upload(bgx_net* n, const float* W1, const float* b1, const float* w2, const float* b2) {
+    std::vector<uint16_t> frag;
+    std::vector<float> rowc;
+    build_fragments(W1, b1, w2, frag, rowc);
+    HIP_TRY(hipMemcpy(n->W1, W1, 128 * 198 * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(n->b1, b1, 128 * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(n->w2, w2, 128 * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(n->wfrag, frag.data(), frag.size() * 2, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(n->rowc, rowc.data(), rowc.size() * 4, hipMemcpyHostToDevice));
+    n->b2 = b2[0];
+    return BGX_OK;
+}
+
+struct bgx_engine {
+    int device = 0;
+    bgx_config cfg{};
+    bgx_net* net = nullptr;
+    bgx::EngineDev d{};
+    hipStream_t last = nullptr;
+    // device buffers
+    uint32_t* rows = nullptr;
+    float* V = nullptr;
+    int32_t* cand_off = nullptr;
+    int32_t* cand_cnt = nullptr;
+    unsigned* ctr = nullptr;   // [0] flat, [1] reply, [2] ovf, [3] ep, [4] err
+    unsigned long long* stats = nullptr;
+    int32_t* sel = nullptr;
+    uint32_t* reply_rows = nullptr;
+    float* reply_V = nullptr;
+    int32_t* job_off = nullptr;
+    int32_t* job_cnt = nullptr;
+    float* job_val = nullptr;
+    int jobs_cap = 0, reply_cap = 0, cand_cap = 0;
+    int32_t* ovf_list = nullptr;
+    int ovf_cap = 0;
+    uint32_t* ws = nullptr;
+    int ws_waves = 0, ws_slots = 0;
+    // harvest
+    uint32_t* out_records = nullptr;
+    int out_cap = 0;
+    int32_t* d_offs = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // pairs: movegen, mlp
+    std::vector<int> ev_kind;
+    double ms_mg = 0, ms_mlp = 0;
+    int n_mg = 0, n_mlp = 0;
+};
+
+extern "C" {
+
+int bgx_abi_version(void) { return BGX_ABI_VERSION; }
+const char* bgx_last_error(void) { return g_err.c_str(); }
+
+int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t* d_dice, int n,
+                uint8_t* d_out_boards, int32_t* d_out_count, int cap, void* stream) {
+    if (n < 0 || cap < 0) return fail(BGX_E_ARG, "bgx_movegen: n=%d cap=%d", n, cap);
+    if (n == 0) return BGX_OK;
+    if (!d_boards || !d_player || !d_dice || !d_out_count || (cap > 0 && !d_out_boards))
+        return fail(BGX_E_ARG, "bgx_movegen: null pointer");
+    // per-call scratch for the overflow path (kept across calls)
+    static unsigned* ctr = nullptr;
+    static int32_t* ovf = nullptr;
+    static uint32_t* ws = nullptr;
+    static int cur_dev = -1;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    const int ovf_cap = 1 << 16, ws_waves = 64, ws_slots = 16384;
+    if (!ctr || cur_dev != dev) {
+        if (dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
+            return BGX_E_HIP;
+        HIP_TRY(hipMemset(ctr, 0, 32));
+        cur_dev = dev;
+    }
+    bgx::MovegenArgs a{};
+    a.n_jobs = n;
+    a.in_mode = bgx::IN_U8;
+    a.in_u8 = d_boards;
+    a.in_player = d_player;
+    a.in_dice = d_dice;
+    a.out_mode = bgx::OUT_U8;
+    a.cap = cap;
+    a.out_u8 = d_out_boards;
+    a.out_count = d_out_count;
+    a.ovf_count = ctr;
+    a.ovf_list = ovf;
+    a.ovf_cap = ovf_cap;
+    a.ws_global = ws;
+    a.ws_waves = ws_waves;
+    a.ws_slots = ws_slots;
+    a.ws_words_per_wave = (size_t)5 * ws_slots;
+    a.err_flags = ctr + 1;
+    HIP_TRY(bgx_launch_movegen(&a, (hipStream_t)stream));
+    return BGX_OK;
+}
+
+int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d_out, int layout,
+               void* stream) {
+    if (n < 0 || (layout != 0 && layout != 1)) return fail(BGX_E_ARG, "bgx_encode: n=%d layout=%d", n, layout);
+    if (n == 0) return BGX_OK;
+    if (!d_boards || !d_player || !d_out) return fail(BGX_E_ARG, "bgx_encode: null pointer");
+    HIP_TRY(bgx_launch_encode(d_boards, d_player, n, d_out, layout, (hipStream_t)stream));
+    return BGX_OK;
+}
+
+int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream) {
+    if (n < 0) return fail(BGX_E_ARG, "bgx_pack: n=%d", n);
+    HIP_TRY(bgx_launch_pack(d_boards, d_player, n, d_packed, (hipStream_t)stream));
+    return BGX_OK;
+}
+
+int bgx_unpack(const uint32_t* d_packed, int n, uint8_t* d_boards, void* stream) {
+    if (n < 0) return fail(BGX_E_ARG, "bgx_unpack: n=%d", n);
+    HIP_TRY(bgx_launch_unpack(d_packed, n, d_boards, (hipStream_t)stream));
+    return BGX_OK;
+}
+
+int bgx_net_create(const float* h_W1, const float* h_b1, const float* h_w2, const float* h_b2,
+                   bgx_net** out) {
+    if (!h_W1 || !h_b1 || !h_w2 || !h_b2 || !out) return fail(BGX_E_ARG, "bgx_net_create: null pointer");
+    bgx_net* n = new bgx_net();
+    if (dalloc(&n->W1, 128 * 198) || dalloc(&n->b1, 128) || dalloc(&n->w2, 128) ||
+        dalloc(&n->wfrag, NFRAG) || dalloc(&n->rowc, 128 * 4)) {
+        bgx_net_destroy(n);
+        return BGX_E_HIP;
+    }
+    int rc = net_upload(n, h_W1, h_b1, h_w2, h_b2);
+    if (rc) {
+        bgx_net_destroy(n);
+        return rc;
+    }
+    *out = n;
+    return BGX_OK;
+}
+
+int bgx_net_destroy(bgx_net* n) {
+    if (!n) return BGX_OK;
+    hipFree(n->W1);
+    hipFree(n->b1);
+    hipFree(n->w2);
+    hipFree(n->wfrag);
+    hipFree(n->rowc);
+    hipFree(n->scratch);
+    delete n;
+    return BGX_OK;
+}
+
+int bgx_value(const bgx_net* net, const float* d_x, int n, float* d_out, void* stream) {
+    if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value: bad arguments");
+    if (n == 0) return BGX_OK;
+    HIP_TRY(bgx_launch_value_f32(d_x, n, net->W1, net->b1, net->w2, net->b2, d_out, (hipStream_t)stream));
+    return BGX_OK;
+}
+
+int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t* d_player, int n,
+                     float* d_out, void* stream) {
+    bgx_net* net = const_cast<bgx_net*>(cnet);
+    if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value_boards: bad arguments");
+    if (n == 0) return BGX_OK;
+    if (net->scratch_n < n) {
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        hipFree(net->scratch);
+        net->scratch = nullptr;
+        if (dalloc(&net->scratch, (size_t)n * 8)) return BGX_E_HIP;
+        net->scratch_n = n;
+    }
+    HIP_TRY(bgx_launch_pack(d_boards, d_player, n, net->scratch, (hipStream_t)stream));
+    bgx::MlpArgs m{};
+    m.rows = net->scratch;
+    m.n_rows = n;
+    m.out = d_out;
+    m.wfrag = net->wfrag;
+    m.rowc = net->rowc;
+    m.b2 = net->b2;
+    HIP_TRY(bgx_launch_mlp(&m, (hipStream_t)stream));
+    return BGX_OK;
+}
+
+void bgx_config_default(bgx_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->lanes = 4096;
+    c->lane_base = 0;
+    c->seed = 0;
+    c->ply = 1;
+    c->k_top = 4;
+    c->alpha = 1.0f;
+    c->beta = 0.9f;
+    c->max_steps = 300;
+    c->max_legal = 500;
+    c->ring = 640;
+    c->ep_cap = 0;   // 0 = derived from lanes
+    c->cand_per_lane = 256;
+    c->reply_per_lane = 0;   // 0 = derived from k_top
+}
+
+int bgx_engine_destroy(bgx_engine* e) {
+    if (!e) return BGX_OK;
+    hipSetDevice(e->device);
+    hipDeviceSynchronize();
+    void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
+                  e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
+                  e->d_offs, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
+                  e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
+    for (void* p : ps) hipFree(p);
+    for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+    bgx_net_destroy(e->net);
+    delete e;
+    return BGX_OK;
+}
+
+int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
+    if (!cfg || !out) return fail(BGX_E_ARG, "bgx_engine_create: null pointer");
+    if (cfg->lanes <= 0 || cfg->lanes > (1 << 24)) return fail(BGX_E_ARG, "lanes=%d", cfg->lanes);
+    if (cfg->ply != 1 && cfg->ply != 2) return fail(BGX_E_ARG, "ply=%d (1 or 2)", cfg->ply);
+    if (cfg->ply == 2 && cfg->k_top != 4 && cfg->k_top != 0)
+        return fail(BGX_E_ARG, "k_top=%d (4 = reference, 0 = all)", cfg->k_top);
+    if (cfg->max_steps <= 0 || cfg->max_legal <= 0) return fail(BGX_E_ARG, "max_steps/max_legal");
+    if (cfg->ring < cfg->max_steps + 1) return fail(BGX_E_ARG, "ring=%d < max_steps+1", cfg->ring);
+    HIP_TRY(hipSetDevice(device));
+    bgx_engine* e = new bgx_engine();
+    e->device = device;
+    e->cfg = *cfg;
+    const int L = cfg->lanes;
+    e->cand_cap = L * (cfg->cand_per_lane > 0 ? cfg->cand_per_lane : 256);
+    const int ep_cap = cfg->ep_cap > 0 ? cfg->ep_cap : 4 * L + 1024;
+    int rc = BGX_OK;
+    bgx::EngineDev& d = e->d;
+#define ALLOC(p, n) \
+    if (!rc) rc = dalloc(&(p), (size_t)(n))
+    ALLOC(e->rows, (size_t)(L + e->cand_cap) * 8);
+    ALLOC(e->V, (size_t)(L + e->cand_cap));
+    ALLOC(e->cand_off, L);
+    ALLOC(e->cand_cnt, L);
+    ALLOC(e->ctr, 16);
+    ALLOC(e->stats, 8);
+    ALLOC(d.player, L);
+    ALLOC(d.dice, 2 * L);
+    ALLOC(d.step, L);
+    ALLOC(d.flags, L);
+    ALLOC(d.epi, L);
+    ALLOC(d.rng, L);
+    ALLOC(d.rec_count, L);
+    ALLOC(d.ep_first, L);
+    ALLOC(d.harv, L);
+    ALLOC(d.ring, (size_t)L * cfg->ring * bgx::REC_WORDS);
+    ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
+    e->ovf_cap = 1 << 16;
+    e->ws_waves = 128;
+    e->ws_slots = 16384;
+    ALLOC(e->ovf_list, e->ovf_cap);
+    ALLOC(e->ws, (size_t)e->ws_waves * 5 * e->ws_slots);
+    if (cfg->ply == 2) {
+        e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
+        const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
+        e->reply_cap = L * per_lane;
+        ALLOC(e->sel, 4 * L);
+        ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
+        ALLOC(e->reply_V, e->reply_cap);
+        ALLOC(e->job_off, e->jobs_cap);
+        ALLOC(e->job_cnt, e->jobs_cap);
+        ALLOC(e->job_val, e->jobs_cap);
+    }
+#undef ALLOC
+    if (rc) {
+        bgx_engine_destroy(e);
+        return rc;
+    }
+    if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess) {
+        bgx_engine_destroy(e);
+        return fail(BGX_E_HIP, "hipMemset failed");
+    }
+    d.L = L;
+    d.lane_base = cfg->lane_base;
+    d.seed = cfg->seed;
+    d.temperature = 1.5f;
+    d.max_steps = cfg->max_steps;
+    d.max_legal = cfg->max_legal;
+    d.ply = cfg->ply;
+    d.k_top = cfg->k_top;
+    d.alpha = cfg->alpha;
+    d.beta = cfg->beta;
+    d.rows = e->rows;
+    d.cand_cap = e->cand_cap;
+    d.R = cfg->ring;
+    d.ep_count = e->ctr + 3;
+    d.ep_cap = ep_cap;
+    d.cand_off = e->cand_off;
+    d.cand_cnt = e->cand_cnt;
+    d.V = e->V;
+    d.sel = e->sel;
+    d.job_val = e->job_val;
+    d.flat_count = e->ctr + 0;
+    d.reply_count = e->ctr + 1;
+    d.ovf_count = e->ctr + 2;
+    d.n_jobs2 = cfg->k_top == 4 ? L * 4 * 21 : 0;
+    d.stats = e->stats;
+    d.err_flags = e->ctr + 4;
+    if (bgx_launch_engine_reset(&d, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        bgx_engine_destroy(e);
+        return fail(BGX_E_HIP, "engine reset failed");
+    }
+    *out = e;
+    return BGX_OK;
+}
+
+int bgx_set_weights(bgx_engine* e, const float* h_W1, const float* h_b1, const float* h_w2,
+                    const float* h_b2, float temperature, uint64_t version) {
+    (void)version;
+    if (!e) return fail(BGX_E_ARG, "bgx_set_weights: null engine");
+    if (!(temperature > 0.0f)) return fail(BGX_E_ARG, "temperature=%g", (double)temperature);
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+    if (!e->net) {
+        int rc = bgx_net_create(h_W1, h_b1, h_w2, h_b2, &e->net);
+        if (rc) return rc;
+    } else {
+        int rc = net_upload(e->net, h_W1, h_b1, h_w2, h_b2);
+        if (rc) return rc;
+    }
+    e->d.temperature = temperature;
+    return BGX_OK;
+}
+
+static void mg_common(bgx_engine* e, bgx::MovegenArgs& a) {
+    a.ovf_count = e->ctr + 2;
+    a.ovf_list = e->ovf_list;
+    a.ovf_cap = e->ovf_cap;
+    a.ws_global = e->ws;
+    a.ws_waves = e->ws_waves;
+    a.ws_slots = e->ws_slots;
+    a.ws_words_per_wave = (size_t)5 * e->ws_slots;
+    a.err_flags = e->ctr + 4;
+}
+
+static int timed(bgx_engine* e, int kind, hipStream_t s, bool start) {
+    if (!e->timing) return BGX_OK;
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreate(&ev));
+    HIP_TRY(hipEventRecord(ev, s));
+    e->ev.push_back(ev);
+    e->ev_kind.push_back(start ? kind : -1);
+    return BGX_OK;
+}
+
+int bgx_step(bgx_engine* e, int n_steps, void* stream) {
+    if (!e || n_steps < 0) return fail(BGX_E_ARG, "bgx_step: bad arguments");
+    if (!e->net) return fail(BGX_E_STATE, "bgx_step: bgx_set_weights first");
+    if (n_steps > e->cfg.ring - e->cfg.max_steps)
+        return fail(BGX_E_ARG, "bgx_step: n_steps=%d > ring - max_steps = %d (harvest more often)", n_steps,
+                    e->cfg.ring - e->cfg.max_steps);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    e->last = s;
+    const int L = e->cfg.lanes;
+    for (int it = 0; it < n_steps; ++it) {
+        HIP_TRY(hipMemsetAsync(e->ctr, 0, 8, s));   // flat + reply counters
+        bgx::MovegenArgs a{};
+        a.n_jobs = L;
+        a.in_mode = bgx::IN_PACKED;
+        a.in_packed = e->rows;
+        a.in_player = e->d.player;
+        a.in_dice = e->d.dice;
+        a.out_mode = bgx::OUT_PACKED_FLAT;
+        a.out_packed = e->rows + (size_t)L * 8;
+        a.flat_count = e->ctr + 0;
+        a.flat_cap = e->cand_cap;
+        a.job_off = e->cand_off;
+        a.job_cnt = e->cand_cnt;
+        mg_common(e, a);
+        if (timed(e, 0, s, true)) return BGX_E_HIP;
+        HIP_TRY(bgx_launch_movegen(&a, s));
+        if (timed(e, 0, s, false)) return BGX_E_HIP;
+
+        bgx::MlpArgs m{};
+        m.rows = e->rows;
+        m.n_rows = L;
+        m.n_rows_dev = e->ctr + 0;
+        m.out = e->V;
+        m.wfrag = e->net->wfrag;
+        m.rowc = e->net->rowc;
+        m.b2 = e->net->b2;
+        if (timed(e, 1, s, true)) return BGX_E_HIP;
+        HIP_TRY(bgx_launch_mlp(&m, s));
+        if (timed(e, 1, s, false)) return BGX_E_HIP;
+
+        if (e->cfg.ply == 2) {
+            bgx::MovegenArgs b{};
+            b.in_mode = bgx::IN_TWOPLY;
+            b.in_packed = e->rows;
+            if (e->cfg.k_top == 4) {
+                HIP_TRY(bgx_launch_topk(&e->d, s));
+                b.n_jobs = L * 4 * 21;
+                b.in_rows = e->sel;
+            } else {
+                b.n_jobs = 0;
+                b.n_jobs_dev = e->ctr + 0;
+                b.jobs_per_dev_unit = 21;
+                b.in_rows = nullptr;
+                b.in_row_base = L;
+            }
+            b.out_mode = bgx::OUT_PACKED_FLAT;
+            b.out_packed = e->reply_rows;
+            b.flat_count = e->ctr + 1;
+            b.flat_cap = e->reply_cap;
+            b.job_off = e->job_off;
+            b.job_cnt = e->job_cnt;
+            mg_common(e, b);
+            if (timed(e, 0, s, true)) return BGX_E_HIP;
+            HIP_TRY(bgx_launch_movegen(&b, s));
+            if (timed(e, 0, s, false)) return BGX_E_HIP;
+            bgx::MlpArgs r{};
+            r.rows = e->reply_rows;
+            r.n_rows = 0;
+            r.n_rows_dev = e->ctr + 1;
+            r.out = e->reply_V;
+            r.wfrag = e->net->wfrag;
+            r.rowc = e->net->rowc;
+            r.b2 = e->net->b2;
+            if (timed(e, 1, s, true)) return BGX_E_HIP;
+            HIP_TRY(bgx_launch_mlp(&r, s));
+            if (timed(e, 1, s, false)) return BGX_E_HIP;
+            if (e->cfg.k_top == 4) {
+                HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, L * 4 * 21, nullptr, 0, L * 4 * 21,
+                                        e->job_val, s));
+            } else {
+                HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, 0, e->ctr + 0, 21, e->jobs_cap,
+                                        e->job_val, s));
+            }
+        }
+        HIP_TRY(bgx_launch_engine_step(&e->d, s));
+    }
+    return BGX_OK;
+}
+
+static int check_flags(bgx_engine* e) {
+    unsigned f = 0;
+    HIP_TRY(hipMemcpy(&f, e->ctr + 4, 4, hipMemcpyDeviceToHost));
+    if (f) {
+        HIP_TRY(hipMemset(e->ctr + 4, 0, 4));
+        return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
+                    "workspace, 8 experience ring, 16 episode list)", f);
+    }
+    return BGX_OK;
+}
+
+int bgx_sync(bgx_engine* e) {
+    if (!e) return fail(BGX_E_ARG, "bgx_sync: null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->last));
+    return check_flags(e);
+}
+
+int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
+    if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest: null pointer");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipStreamSynchronize(e->last));
+    HIP_TRY(hipStreamSynchronize(s));
+    int rc = check_flags(e);
+    if (rc) return rc;
+    unsigned n_eps = 0;
+    HIP_TRY(hipMemcpy(&n_eps, e->ctr + 3, 4, hipMemcpyDeviceToHost));
+    if ((int)n_eps > e->d.ep_cap) n_eps = (unsigned)e->d.ep_cap;
+    std::vector<uint32_t> hdr((size_t)n_eps * bgx::EP_WORDS);
+    if (n_eps) HIP_TRY(hipMemcpy(hdr.data(), e->d.ep_list, hdr.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> offs(n_eps + 1, 0);
+    for (unsigned i = 0; i < n_eps; ++i) offs[i + 1] = offs[i] + (int32_t)hdr[(size_t)i * bgx::EP_WORDS + 3];
+    const int total = offs[n_eps];
+    if (total > e->out_cap) {
+        hipFree(e->out_records);
+        e->out_records = nullptr;
+        const int cap = total + total / 2 + 1024;
+        if (dalloc(&e->out_records, (size_t)cap * bgx::REC_WORDS)) return BGX_E_HIP;
+        e->out_cap = cap;
+    }
+    if ((int)offs.size() > 0) {
+        hipFree(e->d_offs);
+        e->d_offs = nullptr;
+        if (dalloc(&e->d_offs, offs.size())) return BGX_E_HIP;
+        HIP_TRY(hipMemcpy(e->d_offs, offs.data(), offs.size() * 4, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(bgx_launch_gather(&e->d, e->d.ep_list, e->d_offs, (int)n_eps, e->out_records, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemset(e->ctr + 3, 0, 4));
+    out->n_episodes = (int)n_eps;
+    out->n_records = total;
+    out->d_headers = e->d.ep_list;
+    out->d_records = e->out_records;
+    return BGX_OK;
+}
+
+int bgx_get_stats(bgx_engine* e, bgx_stats* out) {
+    if (!e || !out) return fail(BGX_E_ARG, "bgx_get_stats: null pointer");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+    unsigned long long st[8];
+    HIP_TRY(hipMemcpy(st, e->stats, sizeof(st), hipMemcpyDeviceToHost));
+    out->env_steps = st[0];
+    out->decisions = st[1];
+    out->episodes = st[2];
+    out->value_rows = st[3];
+    out->movegen_jobs = st[4];
+    out->fallback_jobs = st[5];
+    return BGX_OK;
+}
+
+int bgx_set_timing(bgx_engine* e, int enabled) {
+    if (!e) return fail(BGX_E_ARG, "bgx_set_timing: null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+    for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+    e->ev.clear();
+    e->ev_kind.clear();
+    e->ms_mg = e->ms_mlp = 0;
+    e->n_mg = e->n_mlp = 0;
+    e->timing = enabled != 0;
+    return BGX_OK;
+}
+
+int bgx_get_timing(bgx_engine* e, double* ms_movegen, int* n_movegen, double* ms_mlp, int* n_mlp) {
+    if (!e) return fail(BGX_E_ARG, "bgx_get_timing: null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+    for (size_t i = 0; i + 1 < e->ev.size(); i += 2) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
+        if (e->ev_kind[i] == 0) { e->ms_mg += ms; e->n_mg++; }
+        else { e->ms_mlp += ms; e->n_mlp++; }
+    }
+    for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+    e->ev.clear();
+    e->ev_kind.clear();
+    if (ms_movegen) *ms_movegen = e->ms_mg;
+    if (n_movegen) *n_movegen = e->n_mg;
+    if (ms_mlp) *ms_mlp = e->ms_mlp;
+    if (n_mlp) *n_mlp = e->n_mlp;
+    return BGX_OK;
+}
+
+}  // extern "C"

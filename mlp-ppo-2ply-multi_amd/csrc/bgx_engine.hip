@@ -1,0 +1,429 @@
+// bgx_engine.hip — K4 lane step (select, apply, rewards, records, refill) and
+// the 2-ply reductions (K5 top-k / top-5).
+//
+// One thread per game lane. The lane step restates, per lane:
+//   Worker.play_episode (src/multi/worker.py:78-174): pass when no legal
+//     move, else V over [obs; candidates], softmax(V[1:]/T) sampling;
+//   BackgammonEnv.step (src/environments/backgammon_env.py:130-221): apply,
+//     win / gammon / backgammon (2.5 / 2.0 / 1.0), once-per-player close-out
+//     (+0.30) and 5-prime (+0.20) shaping summed in fp32, flip, re-roll;
+//   BackgammonEnv.reset (backgammon_env.py:92-128): starter roll until not a
+//     double (higher first die -> PLAYER1), first roll re-rolled until not a
+//     double; episodes end at done or MAX_TIMESTEPS = 300 env steps.
+// 2-ply (src/multi/two_ply.py:44-150 + its worker hook 153-193): top-4 by
+//   1-ply V, score = alpha*S - beta*sum_rolls P(roll) * mean(top-5 replies),
+//   softmax(score/T) over the four; fewer than four moves fall back to 1-ply.
+// Dice / sampling randomness: Philox4x32-10 keyed by (seed, global lane id).
+#include "bgx_device.h"
+#include "bgx_kernels.h"
+
+namespace bgx {
+
+__constant__ float kRollProb[21] = {
+    1.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 1.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 2.f / 36,
+    1.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 1.f / 36, 2.f / 36, 2.f / 36, 1.f / 36, 2.f / 36, 1.f / 36};
+__constant__ double kRollProbD[21] = {
+    1. / 36, 2. / 36, 2. / 36, 2. / 36, 2. / 36, 2. / 36, 1. / 36, 2. / 36, 2. / 36, 2. / 36, 2. / 36,
+    1. / 36, 2. / 36, 2. / 36, 2. / 36, 1. / 36, 2. / 36, 2. / 36, 1. / 36, 2. / 36, 1. / 36};
+
+BGX_DEV uint64_t lane_key(uint64_t seed, uint32_t gid) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(gid + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct LaneRng {
+    uint64_t key, ctr;
+    BGX_DEV u32x4 next() { return philox(key, 0x5EED0000ull, ctr++); }
+    BGX_DEV void roll(int& a, int& b) {
+        u32x4 r = next();
+        a = die_from(r.x);
+        b = die_from(r.y);
+    }
+};
+
+// packed initial board (immutable_board.py:27-70): P1 {0:2, 11:5, 16:3, 18:5}, P2 {23:2, 12:5, 7:3, 5:5}
+BGX_DEV void initial_packed(uint32_t* w) {
+    w[0] = 0x2u;                       // P1 point 0: 2
+    w[1] = 0x5u << 12;                 // P1 point 11: 5
+    w[2] = (0x3u << 0) | (0x5u << 8);  // P1 points 16: 3, 18: 5
+    w[3] = (0x5u << 20) | (0x3u << 28);// P2 points 5: 5, 7: 3
+    w[4] = 0x5u << 16;                 // P2 point 12: 5
+    w[5] = 0x2u << 28;                 // P2 point 23: 2
+    w[6] = 0;
+    w[7] = 0;
+}
+
+BGX_DEV void load_packed(const uint32_t* p, uint32_t* w) {
+    const uint4 x = ((const uint4*)p)[0], y = ((const uint4*)p)[1];
+    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+}
+BGX_DEV void store_packed(uint32_t* p, const uint32_t* w) {
+    ((uint4*)p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    ((uint4*)p)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+BGX_DEV void set_flag(uint32_t* w, int p) { w[6] = (w[6] & 0xFFFFu) | ((uint32_t)p << 16); }
+
+// reset (backgammon_env.py:92-128); returns starter, leaves first dice in d0/d1
+BGX_DEV int new_game(LaneRng& rng, uint32_t* w, int& d0, int& d1) {
+    initial_packed(w);
+    int a, b;
+    do { rng.roll(a, b); } while (a == b);
+    const int starter = a < b ? 1 : 0;
+    do { rng.roll(a, b); } while (a == b);
+    d0 = a;
+    d1 = b;
+    set_flag(w, starter);
+    return starter;
+}
+
+BGX_DEV uint32_t pts_word(const uint32_t* w, int pl, int k) { return pl ? w[3 + k] : w[k]; }
+
+struct Outcome { float reward; int done, win_type, close, prime; };
+
+// env_helper.py:113-242 on a packed board after `pl` moved
+BGX_DEV Outcome judge(const uint32_t* w, int pl, uint32_t& flags) {
+    Outcome o = {0.0f, 0, 0, 0, 0};
+    const uint32_t s6 = w[6];
+    const int op = 1 - pl;
+    const uint32_t off_m = (s6 >> (8 + 4 * pl)) & 15u, off_o = (s6 >> (8 + 4 * op)) & 15u;
+    const uint32_t bar_o = (s6 >> (4 * op)) & 15u;
+    const uint32_t m0 = pts_word(w, pl, 0), m1 = pts_word(w, pl, 1), m2 = pts_word(w, pl, 2);
+    const uint32_t o0 = pts_word(w, op, 0), o1 = pts_word(w, op, 1), o2 = pts_word(w, op, 2);
+    const uint32_t occ_o = occ24(o0, o1, o2);
+    const uint32_t home = pl == 0 ? 0xFC0000u : 0x3Fu;
+    if (off_m >= 15u) {                                            // check_game_over
+        o.done = 1;
+        if (off_o == 0u && ((occ_o & home) || bar_o > 0u)) { o.reward = 2.5f; o.win_type = 3; }
+        else if (off_o == 0u) { o.reward = 2.0f; o.win_type = 2; }
+        else { o.reward = 1.0f; o.win_type = 1; }
+        return o;
+    }
+    const uint32_t g = ge2_24(m0, m1, m2);
+    float r = 0.0f;
+    const bool closed = bar_o > 0u && (g & home) == home;          // is_closed_out
+    if (closed && !(flags & (1u << pl))) {
+        r += 0.30f;
+        flags |= 1u << pl;
+        o.close = 1;
+    }
+    const uint32_t run5 = g & (g >> 1) & (g >> 2) & (g >> 3) & (g >> 4) & 0xFFFFFu;
+    bool prime = false;                                            // made_at_least_five_prime
+    if (run5) {
+        if (pl == 0) {
+            const int s = __ffs(run5) - 1;
+            prime = (occ_o >> (s + 5)) != 0u;
+        } else {
+            const int s = 31 - __clz(run5);
+            prime = (occ_o & ((1u << s) - 1u)) != 0u;
+        }
+    }
+    if (prime && !(flags & (4u << pl))) {
+        r += 0.20f;
+        flags |= 4u << pl;
+        o.prime = 1;
+    }
+    o.reward = r;
+    return o;
+}
+
+__global__ __launch_bounds__(256) void engine_reset_kernel(EngineDev e) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.L) return;
+    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), 0};
+    uint32_t w[8];
+    int d0, d1;
+    const int p = new_game(rng, w, d0, d1);
+    store_packed(e.rows + (size_t)i * 8, w);
+    e.player[i] = (uint8_t)p;
+    e.dice[2 * i] = (uint8_t)d0;
+    e.dice[2 * i + 1] = (uint8_t)d1;
+    e.step[i] = 0;
+    e.flags[i] = 0;
+    e.epi[i] = 0;
+    e.rng[i] = rng.ctr;
+    e.rec_count[i] = 0;
+    e.ep_first[i] = 0;
+    e.harv[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void engine_step_kernel(EngineDev e) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < e.L;
+    int decided = 0, finished = 0;
+    if (live) {
+        LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), e.rng[i]};
+        int p = e.player[i];
+        int steps = e.step[i];
+        uint32_t flags = e.flags[i];
+        uint32_t w[8];
+        load_packed(e.rows + (size_t)i * 8, w);
+        const int n_full = e.cand_cnt[i];
+        const int n = n_full < e.max_legal ? n_full : e.max_legal;
+        const int base = e.L + e.cand_off[i];
+        int d0 = e.dice[2 * i], d1 = e.dice[2 * i + 1];
+        bool done = false;
+        int win_type = 0, winner = -1;
+        if (n == 0) {
+            // pass (backgammon_env.py:139-151): no experience is recorded (worker.py:106-113)
+            p ^= 1;
+            rng.roll(d0, d1);
+        } else {
+            decided = 1;
+            flags |= 16u << p;
+            const float T = e.temperature;
+            int a = -1;
+            const u32x4 ur = rng.next();
+            const float u = unit_from(ur.x);
+            if (e.ply == 2 && e.k_top == 0) {
+                // 2-ply over every candidate: score_k = alpha*V_k - beta*W_k, softmax(score/T)
+                float mx = -INFINITY;
+                for (int k = 0; k < n; ++k) {
+                    double W = 0.0;
+                    const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
+                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
+                    mx = fmaxf(mx, (float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T);
+                }
+                float sum = 0.0f;
+                for (int k = 0; k < n; ++k) {
+                    double W = 0.0;
+                    const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
+                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
+                    sum += __expf((float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T - mx);
+                }
+                const float t = u * sum;
+                float cum = 0.0f;
+                a = n - 1;
+                for (int k = 0; k < n; ++k) {
+                    double W = 0.0;
+                    const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
+                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
+                    cum += __expf((float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T - mx);
+                    if (t < cum) { a = k; break; }
+                }
+            } else if (e.ply == 2 && e.sel[4 * i] >= 0) {
+                // compute_scores_for_boards: score = alpha * S - beta * W (two_ply.py:83-85)
+                float sc[4];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    double W = 0.0;
+                    const float* jv = e.job_val + (size_t)(4 * i + c) * 21;
+                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
+                    const float S = e.V[e.sel[4 * i + c]];
+                    sc[c] = (float)((double)e.alpha * (double)S - (double)e.beta * W) / T;
+                    mx = fmaxf(mx, sc[c]);
+                }
+                float sum = 0.0f, pr[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { pr[c] = __expf(sc[c] - mx); sum += pr[c]; }
+                const float t = u * sum;
+                // first c with t < sum_{k<=c} pr[k] (inverse CDF)
+                float cum = 0.0f;
+                int pick = 3;
+                for (int c = 0; c < 4; ++c) { cum += pr[c]; if (t < cum) { pick = c; break; } }
+                a = e.sel[4 * i + pick] - base;
+            } else {
+                // softmax(V[1:] / T) + Categorical sample (worker.py:137-143)
+                float mx = -INFINITY;
+                for (int k = 0; k < n; ++k) mx = fmaxf(mx, e.V[base + k] / T);
+                float sum = 0.0f;
+                for (int k = 0; k < n; ++k) sum += __expf(e.V[base + k] / T - mx);
+                const float t = u * sum;
+                float cum = 0.0f;
+                a = n - 1;
+                for (int k = 0; k < n; ++k) {
+                    cum += __expf(e.V[base + k] / T - mx);
+                    if (t < cum) { a = k; break; }
+                }
+            }
+            uint32_t nb[8];
+            load_packed(e.rows + (size_t)(base + a) * 8, nb);
+            const int mover = p;
+            const Outcome o = judge(nb, mover, flags);
+            done = o.done;
+            if (done) { win_type = o.win_type; winner = mover; }
+            else { p ^= 1; rng.roll(d0, d1); }
+            // experience record (worker.py:149-156; Experience, episode.py:5-46)
+            const uint32_t rec = e.rec_count[i];
+            if (rec - e.harv[i] >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
+            uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
+            uint32_t before[8];
+            for (int k = 0; k < 8; ++k) before[k] = w[k];
+            set_flag(before, mover);
+            set_flag(nb, done ? mover : p);
+            store_packed(R, before);
+            store_packed(R + 8, nb);
+            const float vs = e.V[i], va = e.V[base + a];
+            const int dd0 = e.dice[2 * i], dd1 = e.dice[2 * i + 1];
+            uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
+                                     (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
+            uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
+                                         ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
+                                         ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
+                                     e.epi[i], (uint32_t)steps, (uint32_t)(e.lane_base + i));
+            ((uint4*)(R + 16))[0] = tail0;
+            ((uint4*)(R + 16))[1] = tail1;
+            e.rec_count[i] = rec + 1;
+            for (int k = 0; k < 8; ++k) w[k] = nb[k];
+        }
+        ++steps;
+        set_flag(w, p);
+        if (done || steps >= e.max_steps) {
+            finished = 1;
+            const uint32_t slot = atomicAdd(e.ep_count, 1u);
+            if ((int)slot < e.ep_cap) {
+                uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
+                const uint32_t first = e.ep_first[i], nrec = e.rec_count[i] - first;
+                ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), e.epi[i], first, nrec);
+                ((uint4*)h)[1] = make_uint4((uint32_t)steps,
+                                            (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
+                                                (flags << 16),
+                                            0u, 0u);
+            } else {
+                atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
+            }
+            p = new_game(rng, w, d0, d1);
+            steps = 0;
+            flags = 0;
+            e.epi[i] = e.epi[i] + 1;
+            e.ep_first[i] = e.rec_count[i];
+        }
+        store_packed(e.rows + (size_t)i * 8, w);
+        e.player[i] = (uint8_t)p;
+        e.dice[2 * i] = (uint8_t)d0;
+        e.dice[2 * i + 1] = (uint8_t)d1;
+        e.step[i] = steps;
+        e.flags[i] = flags;
+        e.rng[i] = rng.ctr;
+    }
+    // per-wave stats: [0] env steps [1] decisions [2] episodes
+    const uint64_t bl = ballot(live), bd = ballot(decided != 0), bf = ballot(finished != 0);
+    if (lane_id() == 0) {
+        atomicAdd(e.stats + 0, (unsigned long long)__popcll(bl));
+        atomicAdd(e.stats + 1, (unsigned long long)__popcll(bd));
+        atomicAdd(e.stats + 2, (unsigned long long)__popcll(bf));
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned fc = *e.flat_count;
+        unsigned long long rows = (unsigned long long)e.L + fc, jobs = (unsigned long long)e.L;
+        if (e.ply == 2) {
+            rows += *e.reply_count;
+            jobs += e.k_top == 0 ? 21ull * fc : (unsigned long long)e.n_jobs2;
+        }
+        atomicAdd(e.stats + 3, rows);
+        atomicAdd(e.stats + 4, jobs);
+        atomicAdd(e.stats + 5, (unsigned long long)*e.ovf_count);
+    }
+}
+
+// 2-ply: top-4 candidates by 1-ply V (torch.topk, sorted; ties -> lower index)
+__global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.L) return;
+    const int n_full = e.cand_cnt[i];
+    const int n = n_full < e.max_legal ? n_full : e.max_legal;
+    const int base = e.L + e.cand_off[i];
+    if (n < 4) {
+        for (int c = 0; c < 4; ++c) e.sel[4 * i + c] = -1;
+        return;
+    }
+    float bv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {-1, -1, -1, -1};
+    for (int k = 0; k < n; ++k) {
+        const float v = e.V[base + k];
+        if (bi[3] >= 0 && !(v > bv[3])) continue;
+        int pos = 3;
+        while (pos > 0 && (bi[pos - 1] < 0 || v > bv[pos - 1])) {
+            bv[pos] = bv[pos - 1];
+            bi[pos] = bi[pos - 1];
+            --pos;
+        }
+        bv[pos] = v;
+        bi[pos] = k;
+    }
+    for (int c = 0; c < 4; ++c) e.sel[4 * i + c] = base + bi[c];
+}
+
+// 2-ply: per (candidate, roll) job, mean of the top-5 reply values
+// (two_ply.py:133-142); 0 when the opponent has no move (the roll adds nothing)
+__global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
+                                                   const int32_t* __restrict__ job_off,
+                                                   const int32_t* __restrict__ job_cnt, int n_jobs,
+                                                   const unsigned* __restrict__ n_units_dev,
+                                                   int jobs_per_unit, float* __restrict__ out) {
+    int nj = n_jobs;
+    if (n_units_dev) nj += (int)(*n_units_dev) * jobs_per_unit;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nj; j += gridDim.x * blockDim.x) {
+        const int c = job_cnt[j], o = job_off[j];
+        float t0 = -INFINITY, t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY, t4 = -INFINITY;
+        for (int k = 0; k < c; ++k) {
+            const float v = V[o + k];
+            if (!(v > t4)) continue;
+            if (v > t0) { t4 = t3; t3 = t2; t2 = t1; t1 = t0; t0 = v; }
+            else if (v > t1) { t4 = t3; t3 = t2; t2 = t1; t1 = v; }
+            else if (v > t2) { t4 = t3; t3 = t2; t2 = v; }
+            else if (v > t3) { t4 = t3; t3 = v; }
+            else { t4 = v; }
+        }
+        const int m = c < 5 ? c : 5;
+        float s = t0;
+        if (m > 1) s += t1;
+        if (m > 2) s += t2;
+        if (m > 3) s += t3;
+        if (m > 4) s += t4;
+        out[j] = m ? s / (float)m : 0.0f;
+    }
+}
+
+// harvest: copy finished episodes' records out of the lane rings
+__global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
+                                                     const int32_t* __restrict__ offs, int n_eps,
+                                                     uint32_t* __restrict__ out) {
+    const int ep = blockIdx.x;
+    if (ep >= n_eps) return;
+    const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
+    const int lane = (int)h[0] - e.lane_base;
+    const uint32_t first = h[2], nrec = h[3];
+    const size_t words = (size_t)nrec * REC_WORDS;
+    for (size_t q = threadIdx.x; q < words; q += blockDim.x) {
+        const uint32_t r = (uint32_t)(q / REC_WORDS), k = (uint32_t)(q % REC_WORDS);
+        const uint32_t slot = (first + r) % (uint32_t)e.R;
+        out[((size_t)offs[ep] + r) * REC_WORDS + k] = e.ring[((size_t)lane * e.R + slot) * REC_WORDS + k];
+    }
+    if (threadIdx.x == 0) atomicMax(e.harv + lane, first + nrec);
+}
+
+}  // namespace bgx
+
+extern "C" hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::engine_reset_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);
+    return hipGetLastError();
+}
+extern "C" hipError_t bgx_launch_engine_step(const bgx::EngineDev* e, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::engine_step_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);
+    return hipGetLastError();
+}
+extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::topk_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);
+    return hipGetLastError();
+}
+extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt,
+                                      int n_jobs, const unsigned* n_units_dev, int jobs_per_unit,
+                                      int max_jobs, float* out, hipStream_t stream) {
+    if (max_jobs <= 0) return hipSuccess;
+    int blocks = (max_jobs + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
+                       n_units_dev, jobs_per_unit, out);
+    return hipGetLastError();
+}
+extern "C" hipError_t bgx_launch_gather(const bgx::EngineDev* e, const uint32_t* headers,
+                                        const int32_t* offsets, int n_eps, uint32_t* out,
+                                        hipStream_t stream) {
+    if (n_eps <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bgx::gather_kernel, dim3(n_eps), dim3(256), 0, stream, *e, headers, offsets, n_eps,
+                       out);
+    return hipGetLastError();
+}

@@ -1,0 +1,123 @@
+// bgx_kernels.h — launch-argument structs shared by the kernels and the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BGX_ERRF_FLAT_OVERFLOW 1u       // flat reply buffer too small
+#define BGX_ERRF_OVF_LIST 2u            // overflow job list too small
+#define BGX_ERRF_FALLBACK_OVERFLOW 4u   // a job outgrew the global workspace
+#define BGX_ERRF_RING_OVERFLOW 8u       // experience ring overwritten before harvest
+#define BGX_ERRF_EPISODE_LIST 16u       // finished-episode list full
+
+namespace bgx {
+
+enum InMode { IN_U8 = 0, IN_PACKED = 1, IN_TWOPLY = 2 };
+enum OutMode { OUT_U8 = 0, OUT_PACKED_SLOT = 1, OUT_PACKED_FLAT = 2 };
+
+struct MovegenArgs {
+    int n_jobs;                  // host job count (added to the device count below)
+    const unsigned* n_jobs_dev;  // optional: device count of "units"
+    int jobs_per_dev_unit;       //   ... each giving this many jobs (21 for 2-ply rows)
+    int in_mode;
+    const uint8_t* in_u8;        // IN_U8: [n][52]
+    const uint32_t* in_packed;   // IN_PACKED: [n][8]; IN_TWOPLY: candidate rows [*][8]
+    const uint8_t* in_player;    // [n]
+    const uint8_t* in_dice;      // [n][2]
+    const int32_t* in_rows;      // IN_TWOPLY: [n/21] candidate row (or -1 = skip);
+    int in_row_base;             //   if in_rows == nullptr: row = in_row_base + job / 21
+    int out_mode;
+    int cap;                     // per-job output capacity (U8 / SLOT)
+    uint8_t* out_u8;             // [n][cap][52]
+    uint32_t* out_packed;        // SLOT: [n][cap][8]; FLAT: [flat_cap][8]
+    int32_t* out_count;          // [n] full record count (U8 / SLOT)
+    unsigned* flat_count;        // FLAT: running row count
+    int flat_cap;
+    int32_t* job_off;            // FLAT: [n]
+    int32_t* job_cnt;            // FLAT: [n]
+    // overflow handling (doubles whose frontier outgrows the LDS slice)
+    unsigned* ovf_count;
+    int32_t* ovf_list;
+    int ovf_cap;
+    uint32_t* ws_global;         // [ws_waves][ws_words_per_wave]
+    int ws_waves;
+    int ws_slots;                // power of two
+    size_t ws_words_per_wave;    // >= 5 * ws_slots
+    unsigned* err_flags;
+};
+
+// Split-fp16 MLP weights in MFMA fragment order (see bgx_mlp.hip).
+struct MlpArgs {
+    const uint32_t* rows;        // packed boards [n][8] (flag in w[6] bit 16)
+    const unsigned* n_rows_dev;  // if non-null: row count read on device
+    int n_rows;                  // else: row count
+    float* out;                  // [n] V
+    const uint4* wfrag;          // [2][4][13][64] fragments (16 B each)
+    const float* rowc;           // [128][4]: inv_scale, w2, b1*scale, 0
+    float b2;
+};
+
+// Self-play lane state (one engine per device), structure of arrays.
+constexpr int REC_WORDS = 24;   // experience record: 96 B
+constexpr int EP_WORDS = 8;     // episode header: 32 B
+
+struct EngineDev {
+    int L;                       // lanes on this engine
+    int lane_base;               // global id of lane 0 (RNG streams keyed by global id)
+    uint64_t seed;
+    float temperature;
+    int max_steps;               // MAX_TIMESTEPS = 300 (config/configuration.py:4)
+    int max_legal;               // max_legal_moves = 500 (backgammon_env.py:35)
+    int ply;                     // 1 or 2
+    int k_top;                   // 4 (two_ply.py:67-70) or 0 = all candidates
+    float alpha, beta;           // 1.0, 0.9 (two_ply.py:44-50)
+    uint32_t* rows;              // [L + cand_cap][8]: lane boards (obs rows) then candidates
+    int cand_cap;
+    uint8_t* player;             // [L]
+    uint8_t* dice;               // [L][2]
+    int32_t* step;               // [L] env steps in the current episode (passes included)
+    uint32_t* flags;             // [L] bit0/1 close-out given P1/P2, bit2/3 prime given, bit4/5 decided
+    uint32_t* epi;               // [L] episode counter
+    uint64_t* rng;               // [L] Philox counter
+    uint32_t* rec_count;         // [L] records written (absolute)
+    uint32_t* ep_first;          // [L] first record of the current episode
+    uint32_t* harv;              // [L] records harvested (absolute)
+    uint32_t* ring;              // [L][R][REC_WORDS]
+    int R;
+    uint32_t* ep_list;           // [ep_cap][EP_WORDS]
+    unsigned* ep_count;
+    int ep_cap;
+    // per-step inputs
+    const int32_t* cand_off;     // [L] offset of the lane's candidates after row L
+    const int32_t* cand_cnt;     // [L] full candidate count
+    const float* V;              // [L + cand rows] values
+    int32_t* sel;                // [L * 4] 2-ply: candidate rows chosen by 1-ply V (or -1)
+    const float* job_val;        // [L * 4 * 21] 2-ply: top-5 mean per (candidate, roll)
+    const unsigned* flat_count;  // candidate rows this step (device)
+    const unsigned* reply_count; // 2-ply reply rows this step (device)
+    const unsigned* ovf_count;   // jobs sent to the fallback path this step (device)
+    int n_jobs2;                 // 2-ply jobs this step when k_top = 4
+    unsigned long long* stats;   // [8] env steps, decisions, episodes, value rows, movegen jobs, fallback
+    unsigned* err_flags;
+};
+
+}  // namespace bgx
+
+extern "C" {
+hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream_t stream);
+hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t stream);
+hipError_t bgx_launch_encode(const uint8_t* boards, const uint8_t* player, int n, float* out,
+                             int layout, hipStream_t stream);
+hipError_t bgx_launch_value_f32(const float* x, int n, const float* W1, const float* b1,
+                                const float* w2, float b2, float* out, hipStream_t stream);
+hipError_t bgx_launch_pack(const uint8_t* boards, const uint8_t* player, int n, uint32_t* out,
+                           hipStream_t stream);
+hipError_t bgx_launch_unpack(const uint32_t* packed, int n, uint8_t* out, hipStream_t stream);
+hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream_t stream);
+hipError_t bgx_launch_engine_step(const bgx::EngineDev* e, hipStream_t stream);
+hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream);
+hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt, int n_jobs,
+                           const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
+                           hipStream_t stream);
+hipError_t bgx_launch_gather(const bgx::EngineDev* e, const uint32_t* headers, const int32_t* offsets,
+                             int n_eps, uint32_t* out, hipStream_t stream);
+}

@@ -1,0 +1,136 @@
+"""GPU parity: libbgx.so kernels vs the reference golden vectors and the CPU oracle.
+
+Bit-exact for move generation (ordered result boards) and encodings; V(s)
+within the 1e-5 tolerance of BASELINE.json's north_star.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+V_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def bgx_ops():
+    from bgx import ops
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return ops
+
+
+def _run_movegen(ops, boards, player, dice, cap):
+    out, cnt = ops.movegen(torch.from_numpy(np.ascontiguousarray(boards)).cuda(),
+                           torch.from_numpy(np.ascontiguousarray(player)).cuda(),
+                           torch.from_numpy(np.ascontiguousarray(dice)).cuda(), cap=cap)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), cnt.cpu().numpy()
+
+
+def test_movegen_golden_cases(bgx_ops):
+    d = golden("movegen_cases.npz")
+    out, cnt = _run_movegen(bgx_ops, d["boards"], d["player"], d["dice"], cap=1024)
+    for i in range(len(d["boards"])):
+        o0, o1 = d["offsets"][i], d["offsets"][i + 1]
+        assert cnt[i] == o1 - o0, (i, cnt[i], o1 - o0)
+        np.testing.assert_array_equal(out[i, : o1 - o0], d["results"][o0:o1], err_msg=f"case {i}")
+
+
+def test_movegen_golden_digests(bgx_ops):
+    g = golden("movegen_digests.npz")
+    n = len(g["boards"])
+    for s in range(0, n, 2048):
+        e = min(n, s + 2048)
+        out, cnt = _run_movegen(bgx_ops, g["boards"][s:e], g["player"][s:e], g["dice"][s:e], cap=512)
+        for i in range(e - s):
+            assert cnt[i] == g["count"][s + i], s + i
+            h = hashlib.sha256(out[i, : cnt[i]].tobytes()).digest()
+            assert h == g["sha256"][s + i].tobytes(), s + i
+
+
+def _fuzz_positions(seed, n_games):
+    rng = np.random.default_rng(seed)
+    init = golden("movegen_cases.npz")["boards"][0]
+    pos = []
+    for _ in range(n_games):
+        b, pl = init.copy(), int(rng.integers(0, 2))
+        for _s in range(300):
+            pos.append((b.copy(), pl))
+            n, res, _ = orc.movegen(b, pl, int(rng.integers(1, 7)), int(rng.integers(1, 7)))
+            if n:
+                b = res[int(rng.integers(0, min(n, 500)))].copy()
+                if b[50 + pl] >= 15:
+                    break
+            pl = 1 - pl
+    return pos
+
+
+def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops):
+    pos = _fuzz_positions(1234, 40)
+    rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
+    boards = np.stack([p[0] for p in pos for _ in rolls])
+    player = np.array([p[1] for p in pos for _ in rolls], np.uint8)
+    dice = np.array([r for _ in pos for r in rolls], np.uint8)
+    cap = 1024
+    for s in range(0, len(boards), 8192):
+        e = min(len(boards), s + 8192)
+        out, cnt = _run_movegen(bgx_ops, boards[s:e], player[s:e], dice[s:e], cap)
+        for i in range(e - s):
+            n, res, _ = orc.movegen(boards[s + i], player[s + i], *dice[s + i], cap=cap)
+            assert cnt[i] == n, (s + i, cnt[i], n)
+            np.testing.assert_array_equal(out[i, :n], res, err_msg=f"job {s + i}")
+
+
+def test_movegen_zero_and_empty(bgx_ops):
+    out, cnt = bgx_ops.movegen(torch.zeros((0, 52), dtype=torch.uint8).cuda(),
+                               torch.zeros((0,), dtype=torch.uint8).cuda(),
+                               torch.zeros((0, 2), dtype=torch.uint8).cuda())
+    assert out.shape[0] == 0 and cnt.shape[0] == 0
+
+
+def test_encode_bit_exact(bgx_ops):
+    e = golden("encode.npz")
+    b = torch.from_numpy(e["boards"]).cuda()
+    p = torch.from_numpy(e["player"]).cuda()
+    live = bgx_ops.encode(b, p, 0).cpu().numpy()
+    np.testing.assert_array_equal(live.view(np.uint32), e["live"].view(np.uint32))
+    n = len(e["interleaved"])
+    inter = bgx_ops.encode(b[:n], p[:n], 1).cpu().numpy()
+    np.testing.assert_array_equal(inter.view(np.uint32), e["interleaved"].view(np.uint32))
+
+
+def test_pack_unpack_roundtrip(bgx_ops):
+    e = golden("encode.npz")
+    b = torch.from_numpy(e["boards"]).cuda()
+    p = torch.from_numpy(e["player"]).cuda()
+    pk = bgx_ops.pack(b, p)
+    np.testing.assert_array_equal(bgx_ops.unpack(pk).cpu().numpy(), e["boards"])
+    np.testing.assert_array_equal(bgx_ops.packed_player(pk).cpu().numpy(), e["player"])
+
+
+@pytest.mark.parametrize("which", ["seed0", "ckpt"])
+def test_value_paths_within_tol(bgx_ops, which, weights_seed0, weights_ckpt):
+    w = weights_seed0 if which == "seed0" else weights_ckpt
+    v = golden("value.npz")
+    e = golden("encode.npz")
+    ref = v["v_seed0"] if which == "seed0" else v["v_ckpt"]
+    net = bgx_ops.Net(w)
+    got32 = net.value(torch.from_numpy(v["x"]).cuda()).cpu().numpy()
+    assert np.max(np.abs(got32 - ref)) < V_TOL
+    gotb = net.value_boards(torch.from_numpy(e["boards"]).cuda(),
+                            torch.from_numpy(e["player"]).cuda()).cpu().numpy()
+    err = np.max(np.abs(gotb - ref))
+    assert err < V_TOL, err
+    # and against the fp64 oracle on fresh afterstates
+    pos = _fuzz_positions(99, 4)
+    boards = np.stack([p[0] for p in pos])
+    player = np.array([p[1] for p in pos], np.uint8)
+    x = orc.encode_many(boards, player)
+    want = orc.value(w, x)
+    got = net.value_boards(torch.from_numpy(boards).cuda(), torch.from_numpy(player).cuda()).cpu().numpy()
+    assert np.max(np.abs(got - want)) < V_TOL
