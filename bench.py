@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Self-play throughput benchmark (BASELINE.json metric: self-play env steps/sec).
+
+One bench "step" = one env step (one BackgammonEnv.step equivalent, passes
+included) of every lane on every GPU, including the compact Experience
+records, the episode harvest (every --harvest-every steps) and, for N > 1,
+the RCCL gather of the harvested episodes to rank 0. Synthetic data: lanes
+start from the reference's reset and play random-seeded self-play with the
+seeded xavier weights (tests/golden/weights_seed0.npz = torch.manual_seed(0)
+BackgammonPolicyNetwork()), T = 1.5 (ParameterManager version 1).
+
+N = 1:  python bench.py
+N > 1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+            --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mlp-ppo-2ply-multi_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP16_DENSE_PEAK_TFS = 2500.0  # dense fp16 MFMA (no sparsity)
+MLP_FLOP_PER_ROW = 50944     # 2 * (198*128 + 128)  
+MOVEGEN_BYTES_PER_JOB = 54   # parent board + player + dice
+MOVEGEN_BYTES_PER_ROW = 52   # child board written
+METRIC = "self-play env steps/sec (whole node) at 1-ply and 2-ply, 1/2/4/8 MI355X"
+
+
+def load_weights():
+    d = np.load(os.path.join(REPO, "tests", "golden", "weights_seed0.npz"))
+    return {k: d[k] for k in ("W1", "b1", "w2", "b2")}
+
+
+def init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_every, timing):
+    from bgx import Engine
+    from bgx import dist as bdist
+    w = load_weights()
+    if world > 1:
+        w = bdist.broadcast_weights(w)
+    eng = Engine(lanes=lanes, seed=args.seed, ply=ply, k_top=k_top, lane_base=rank * lanes)
+    eng.set_weights(w, temperature=1.5, version=1)
+    gathered = [0, 0]
+
+    def run(n):
+        left = n
+        while left > 0:
+            k = min(harvest_every, left)
+            eng.step(k)
+            h = eng.harvest()
+            if world > 1:
+                eps, recs = bdist.gather_episodes(h, dst=0)
+                if rank == 0:
+                    gathered[0] += eps
+                    gathered[1] += recs
+            left -= k
+
+    run(warmup)
+    eng.sync()
+    s0 = eng.stats()
+    if timing:
+        eng.set_timing(True)
+    barrier(world)
+    t0 = time.perf_counter()
+    run(steps)
+    barrier(world)
+    el = time.perf_counter() - t0
+    s1 = eng.stats()
+    tm = eng.timing() if timing else None
+    eng.close()
+    d = {k: s1[k] - s0[k] for k in s1}
+    return el, d, tm, gathered
+
+
+def cpu_baseline(seconds, threads):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc  # the bench's cpu_baseline leg (oracle = the CPU port)
+    r = orc.selfplay_bench(load_weights(), temperature=1.5, seed=0, n_threads=threads, seconds=seconds)
+    return r
+
+
+def roofline_for(d, tm, el):
+    """Dominant kernel's algorithmic rate over its average launch (HIP events)."""
+    mg_ms, mlp_ms = tm["movegen_ms"], tm["mlp_ms"]
+    out = {}
+    mg_bytes = MOVEGEN_BYTES_PER_JOB * d["movegen_jobs"] + MOVEGEN_BYTES_PER_ROW * d["value_rows"]
+    mg_launch = mg_ms / max(1, tm["movegen_launches"])
+    out["movegen"] = {"bound": "hbm", "achieved": mg_bytes / max(1, tm["movegen_launches"]) / (mg_launch * 1e-3) / 1e9,
+                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "avg_launch_ms": mg_launch,
+                      "launches": tm["movegen_launches"], "share_of_wall": mg_ms * 1e-3 / el}
+    mlp_launch = mlp_ms / max(1, tm["mlp_launches"])
+    mlp_flop = MLP_FLOP_PER_ROW * d["value_rows"] / max(1, tm["mlp_launches"])
+    out["mlp"] = {"bound": "mfma", "achieved": mlp_flop / (mlp_launch * 1e-3) / 1e12, "peak": FP16_DENSE_PEAK_TFS,
+                  "unit": "TFLOP/s", "avg_launch_ms": mlp_launch, "launches": tm["mlp_launches"],
+                  "share_of_wall": mlp_ms * 1e-3 / el}
+    for v in out.values():
+        v["frac"] = v["achieved"] / v["peak"]
+    dom = "movegen" if mg_ms >= mlp_ms else "mlp"
+    r = {k: out[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
+    r["kernel"] = "bgx::movegen_lds_kernel" if dom == "movegen" else "bgx::mlp_kernel"
+    r["traffic"] = None
+    prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            with open(prof) as f:
+                r["traffic"] = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            r["traffic"] = None
+    return r, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--lanes", type=int, default=4096, help="lanes per GPU (configs[1]: 4096)")
+    ap.add_argument("--ply", type=int, default=1)
+    ap.add_argument("--k-top", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--harvest-every", type=int, default=100)
+    ap.add_argument("--two-ply-steps", type=int, default=100, help="extra 2-ply (K=4) measurement; 0 = skip")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=7, help="mirrors src/main.py:86 (7 workers)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = init_dist()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    el, d, tm, gathered = run_engine(args, world, rank, args.ply, args.k_top, args.lanes, args.steps,
+                                     args.warmup, args.harvest_every, timing=True)
+    el = max_over_ranks(el, world)
+    total_steps = sum_over_ranks(d["env_steps"], world)
+    value = total_steps / el
+    roof, kernels = roofline_for(d, tm, el)
+
+    extra = {}
+    if args.two_ply_steps > 0 and args.ply == 1:
+        el2, d2, tm2, _ = run_engine(args, world, rank, 2, 4, args.lanes, args.two_ply_steps, 20,
+                                     args.harvest_every, timing=True)
+        el2 = max_over_ranks(el2, world)
+        tot2 = sum_over_ranks(d2["env_steps"], world)
+        r2, k2 = roofline_for(d2, tm2, el2)
+        extra["two_ply_k4"] = {"value": tot2 / el2, "unit": "env_steps/s", "steps": args.two_ply_steps,
+                               "ms_per_step": el2 / args.two_ply_steps * 1e3,
+                               "value_rows_per_s": sum_over_ranks(d2["value_rows"], world) / el2,
+                               "movegen_jobs_per_s": sum_over_ranks(d2["movegen_jobs"], world) / el2,
+                               "roofline": r2, "kernels": k2}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        r = cpu_baseline(args.cpu_seconds, args.cpu_threads)
+        cpu = {"value": r["steps"] / r["elapsed"], "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
+               "sample": f"{r['threads']} host threads x {r['elapsed']:.1f} s of 1-ply self-play with the CPU "
+                         f"oracle port (oracle/bgref.c; same weights, T=1.5): {r['steps']} env steps, "
+                         f"{r['episodes']} episodes; reference Python 7-worker path measured 2052 env steps/s "
+                         f"in the survey container (BASELINE.md)"}
+
+    sums = {k: sum_over_ranks(d[k], world) for k in ("decisions", "episodes", "value_rows", "fallback_jobs")}
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8 game state + fp16x2-split MFMA (fp32 acc)",
+            "data": "synthetic: random-seeded self-play from the reference reset, seeded xavier weights",
+            "config": {"workload": f"{args.lanes} game lanes per GPU, {args.ply}-ply softmax select"
+                                   + (" (configs[1])" if args.ply == 1 and args.lanes == 4096 else ""),
+                       "lanes_per_gpu": args.lanes, "lanes_total": args.lanes * world, "ply": args.ply,
+                       "harvest_every": args.harvest_every, "parallelism": f"lanes sharded x{world}, "
+                       "RCCL episode gather" if world > 1 else "single GPU"},
+            "decisions_per_s": sums["decisions"] / el,
+            "episodes_per_s": sums["episodes"] / el,
+            "value_rows_per_s": sums["value_rows"] / el,
+            "fallback_jobs": int(sums["fallback_jobs"]),
+            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
+        }
+        if world > 1:
+            line["gathered_episodes"] = gathered[0]
+        line.update(extra)
+        print(json.dumps(line))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -70,6 +70,14 @@ int bgx_value(const bgx_net* net, const float* d_x, int n, float* d_out, void* s
 int bgx_value_boards(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_player, int n,
                      float* d_out, void* stream);
 
+/* compute_weighted_opponent_response (multi/two_ply.py:93-150) in exact mode
+ * (no random.sample of 1-1/2-2/3-3 replies): for n afterstates d_boards and
+ * the player to reply d_opponent, d_out[i] = sum over the 21 rolls of
+ * P(roll) * mean of the top-5 V of the opponent's replies (V with the
+ * opponent's indicator). Synchronizes `stream`. */
+int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
+                double* d_out, void* stream);
+
 /* ---------------- self-play engine ---------------- */
 typedef struct bgx_engine bgx_engine;
 

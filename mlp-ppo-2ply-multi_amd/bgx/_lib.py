@@ -57,6 +57,7 @@ SIGNATURES = {
     "bgx_net_destroy": (c_int, [c_void_p]),
     "bgx_value": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "bgx_value_boards": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "bgx_two_ply": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "bgx_config_default": (None, [ctypes.POINTER(Config)]),
     "bgx_engine_create": (c_int, [c_int, ctypes.POINTER(Config), ctypes.POINTER(c_void_p)]),
     "bgx_engine_destroy": (c_int, [c_void_p]),

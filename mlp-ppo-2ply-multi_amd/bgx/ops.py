@@ -137,3 +137,13 @@ class Net:
         check(lib().bgx_value_boards(self._h, ptr(boards), ptr(player), boards.shape[0], ptr(out),
                                      stream_handle(stream)), "bgx_value_boards")
         return out
+
+    def two_ply(self, boards, opponent, stream=None):
+        """Exact-mode compute_weighted_opponent_response (two_ply.py:93-150) for
+        afterstates [n, 52]; returns float64 W [n]."""
+        boards, opponent = _u8(boards).view(-1, 52), _u8(opponent).view(-1)
+        require_cuda(boards, opponent)
+        out = torch.empty((boards.shape[0],), dtype=torch.float64, device=boards.device)
+        check(lib().bgx_two_ply(self._h, ptr(boards), ptr(opponent), boards.shape[0], ptr(out),
+                                stream_handle(stream)), "bgx_two_ply")
+        return out

@@ -284,6 +284,83 @@ int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t
     return BGX_OK;
 }
 
+int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
+                double* d_out, void* stream) {
+    if (!net || n < 0) return fail(BGX_E_ARG, "bgx_two_ply: bad arguments");
+    if (n == 0) return BGX_OK;
+    if (!d_boards || !d_opponent || !d_out) return fail(BGX_E_ARG, "bgx_two_ply: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    const int jobs = n * 21;
+    const int cap = jobs * 768;   // >= any reply count per (board, roll)
+    uint8_t* mover = nullptr;
+    uint32_t *rows = nullptr, *reply = nullptr, *ws = nullptr;
+    unsigned* ctr = nullptr;
+    int32_t *off = nullptr, *cnt = nullptr, *ovf = nullptr;
+    float *V = nullptr, *jv = nullptr;
+    int rc = BGX_OK;
+    const int ws_waves = 64, ws_slots = 16384, ovf_cap = 1 << 16;
+    if (dalloc(&mover, n) || dalloc(&rows, (size_t)n * 8) || dalloc(&reply, (size_t)cap * 8) ||
+        dalloc(&ctr, 8) || dalloc(&off, jobs) || dalloc(&cnt, jobs) || dalloc(&V, cap) || dalloc(&jv, jobs) ||
+        dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots)) {
+        rc = BGX_E_HIP;
+    }
+    std::vector<uint8_t> hm;
+    if (!rc) {
+        // the candidate board's indicator = the player who just moved = 1 - opponent
+        std::vector<uint8_t> ho(n);
+        if (hipMemcpy(ho.data(), d_opponent, n, hipMemcpyDeviceToHost) != hipSuccess) rc = BGX_E_HIP;
+        hm.resize(n);
+        for (int i = 0; i < n; ++i) hm[i] = (uint8_t)(1 - (ho[i] & 1));
+    }
+    if (!rc && hipMemcpy(mover, hm.data(), n, hipMemcpyHostToDevice) != hipSuccess) rc = BGX_E_HIP;
+    if (!rc && hipMemsetAsync(ctr, 0, 32, s) != hipSuccess) rc = BGX_E_HIP;
+    if (!rc && bgx_launch_pack(d_boards, mover, n, rows, s) != hipSuccess) rc = BGX_E_HIP;
+    if (!rc) {
+        bgx::MovegenArgs b{};
+        b.n_jobs = jobs;
+        b.in_mode = bgx::IN_TWOPLY;
+        b.in_packed = rows;
+        b.in_rows = nullptr;
+        b.in_row_base = 0;
+        b.out_mode = bgx::OUT_PACKED_FLAT;
+        b.out_packed = reply;
+        b.flat_count = ctr;
+        b.flat_cap = cap;
+        b.job_off = off;
+        b.job_cnt = cnt;
+        b.ovf_count = ctr + 2;
+        b.ovf_list = ovf;
+        b.ovf_cap = ovf_cap;
+        b.ws_global = ws;
+        b.ws_waves = ws_waves;
+        b.ws_slots = ws_slots;
+        b.ws_words_per_wave = (size_t)5 * ws_slots;
+        b.err_flags = ctr + 3;
+        if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
+    }
+    if (!rc) {
+        bgx::MlpArgs m{};
+        m.rows = reply;
+        m.n_rows = 0;
+        m.n_rows_dev = ctr;
+        m.out = V;
+        m.wfrag = net->wfrag;
+        m.rowc = net->rowc;
+        m.b2 = net->b2;
+        if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
+    }
+    if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, s) != hipSuccess) rc = BGX_E_HIP;
+    if (!rc && bgx_launch_two_ply_reduce(jv, n, d_out, s) != hipSuccess) rc = BGX_E_HIP;
+    unsigned flags = 0;
+    if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = BGX_E_HIP;
+    void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws};
+    for (void* p : ps) hipFree(p);
+    if (rc) return fail(rc, "bgx_two_ply: HIP failure");
+    if (flags) return fail(BGX_E_CAPACITY, "bgx_two_ply: overflow flags 0x%x", flags);
+    return BGX_OK;
+}
+
 void bgx_config_default(bgx_config* c) {
     std::memset(c, 0, sizeof(*c));
     c->lanes = 4096;

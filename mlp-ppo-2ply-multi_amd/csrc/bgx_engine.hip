@@ -377,6 +377,16 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
     }
 }
 
+// 2-ply W per board: sum over the 21 rolls of P(roll) * top-5 mean (two_ply.py:143-150)
+__global__ __launch_bounds__(256) void two_ply_reduce_kernel(const float* __restrict__ job_val, int n,
+                                                             double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double W = 0.0;
+    for (int r = 0; r < 21; ++r) W += (double)job_val[(size_t)i * 21 + r] * kRollProbD[r];
+    out[i] = W;
+}
+
 // harvest: copy finished episodes' records out of the lane rings
 __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
                                                      const int32_t* __restrict__ offs, int n_eps,
@@ -417,6 +427,13 @@ extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, co
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
                        n_units_dev, jobs_per_unit, out);
+    return hipGetLastError();
+}
+extern "C" hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out,
+                                                 hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bgx::two_ply_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, job_val, n,
+                       out);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_gather(const bgx::EngineDev* e, const uint32_t* headers,

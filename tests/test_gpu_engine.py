@@ -1,0 +1,176 @@
+"""GPU engine parity: every harvested Experience is replayed through the CPU oracle.
+
+The engine's dice and sampling streams cannot match the reference's
+(np.random / torch.distributions), so the check is per transition: the
+recorded (board, mover, dice) must generate — in the oracle, which is pinned
+to the reference — the recorded afterstate at the recorded action index, and
+V(s), V(a), reward, done, win type and shaping flags must equal what the
+oracle computes for that transition (worker.py:101-162, backgammon_env.py:130-221).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+import oracle as orc
+
+pytestmark = pytest.mark.gpu
+V_TOL = 1e-5
+
+
+def _engine(weights, **kw):
+    from bgx import Engine
+    e = Engine(**kw)
+    e.set_weights(weights, temperature=1.5, version=1)
+    return e
+
+
+def _collect(e, steps, chunk=100):
+    from bgx.episodes import decode_records
+    hdrs, recs = [], []
+    done = 0
+    while done < steps:
+        k = min(chunk, steps - done)
+        e.step(k)
+        h = e.harvest()
+        hdrs.append(h.headers.cpu().numpy().astype(np.uint32))
+        recs.append(decode_records(h.records))
+        done += k
+    e.sync()
+    return hdrs, recs
+
+
+def _check_transitions(weights, hdrs, recs, ply):
+    n_checked = 0
+    for hdr, d in zip(hdrs, recs):
+        o = 0
+        for row in hdr:
+            n = int(row[3])
+            flags = 0
+            for k in range(o, o + n):
+                b, mover, dice = d["before"][k], int(d["mover"][k]), d["dice"][k]
+                cnt, res, _ = orc.movegen(b, mover, int(dice[0]), int(dice[1]))
+                assert d["n_moves"][k] == cnt and cnt > 0
+                a = int(d["action"][k])
+                assert 0 <= a < min(cnt, 500)
+                np.testing.assert_array_equal(res[a], d["after"][k])
+                xs = orc.encode_many(np.stack([b, res[a]]), [mover, mover])
+                v = orc.value(weights, xs)
+                assert abs(v[0] - d["v_s"][k]) < V_TOL and abs(v[1] - d["v_a"][k]) < V_TOL
+                # reward / terminal / shaping (env_helper.py:113-242, backgammon_env.py:167-213)
+                after = res[a]
+                if orc.predicate("check_game_over", after, mover):
+                    wt = 3 if orc.predicate("check_for_backgammon", after, mover) else (
+                        2 if orc.predicate("check_for_gammon", after, mover) else 1)
+                    assert d["done"][k] and d["win_type"][k] == wt
+                    assert d["reward"][k] == np.float32({1: 1.0, 2: 2.0, 3: 2.5}[wt])
+                    assert k == o + n - 1
+                else:
+                    assert not d["done"][k]
+                    r = np.float32(0.0)
+                    co = orc.predicate("is_closed_out", after, mover) and not (flags >> mover) & 1
+                    pr = orc.predicate("made_at_least_five_prime", after, mover) and not (flags >> (2 + mover)) & 1
+                    if co:
+                        r = np.float32(r + np.float32(0.30))
+                        flags |= 1 << mover
+                    if pr:
+                        r = np.float32(r + np.float32(0.20))
+                        flags |= 4 << mover
+                    assert bool(d["close_out"][k]) == bool(co) and bool(d["prime"][k]) == bool(pr)
+                    assert d["reward"][k] == r
+                if k > o:   # passes never change the board
+                    np.testing.assert_array_equal(d["before"][k], d["after"][k - 1])
+                n_checked += 1
+            if n:
+                first = d["before"][o]
+                assert d["step"][o] >= 0
+            assert int(row[4]) <= 300
+            assert int(row[4]) == 300 or (n > 0 and d["done"][o + n - 1])
+            o += n
+    return n_checked
+
+
+def test_engine_1ply_transitions_match_oracle(weights_seed0):
+    e = _engine(weights_seed0, lanes=512, seed=11, ply=1)
+    hdrs, recs = _collect(e, 400)
+    assert sum(len(h) for h in hdrs) > 100
+    assert _check_transitions(weights_seed0, hdrs, recs, 1) > 10000
+    st = e.stats()
+    assert st["env_steps"] == 512 * 400
+    e.close()
+
+
+def test_engine_episode_starts_from_reset(weights_seed0):
+    e = _engine(weights_seed0, lanes=256, seed=5, ply=1)
+    hdrs, recs = _collect(e, 300)
+    init = golden("movegen_cases.npz")["boards"][0]
+    for hdr, d in zip(hdrs, recs):
+        o = 0
+        for row in hdr:
+            n = int(row[3])
+            if n and int(row[1]) > 0:   # every episode after the lane's first starts at the reset
+                np.testing.assert_array_equal(d["before"][o], init)
+                assert d["dice"][o][0] != d["dice"][o][1]   # first roll re-rolled off doubles
+            o += n
+    e.close()
+
+
+def test_engine_sampling_distribution(weights_seed0):
+    """chi-square: the first decision of each lane is sampled from softmax(V/T)."""
+    from bgx.episodes import decode_records
+    e = _engine(weights_seed0, lanes=16384, seed=3, ply=1)
+    e.step(1)
+    e.sync()
+    # the first step of every lane is a decision from the initial board
+    e.step(299)
+    h = e.harvest()
+    d = decode_records(h.records)
+    first = d["step"] == 0
+    init = golden("movegen_cases.npz")["boards"][0]
+    groups = {}
+    for k in np.nonzero(first)[0]:
+        if not np.array_equal(d["before"][k], init):
+            continue
+        key = (int(d["mover"][k]), int(d["dice"][k][0]), int(d["dice"][k][1]))
+        groups.setdefault(key, []).append(int(d["action"][k]))
+    from scipy.stats import chisquare
+    tested = 0
+    for (mover, d0, d1), acts in groups.items():
+        if len(acts) < 200:
+            continue
+        cnt, res, _ = orc.movegen(init, mover, d0, d1)
+        v = orc.value(weights_seed0, orc.encode_many(res, [mover] * cnt))
+        p = np.exp((v - v.max()) / 1.5)
+        p /= p.sum()
+        obs = np.bincount(acts, minlength=cnt)
+        assert chisquare(obs, p * len(acts)).pvalue > 1e-4, (mover, d0, d1)
+        tested += 1
+    assert tested >= 3
+    e.close()
+
+
+def test_engine_2ply_k4_transitions(weights_seed0):
+    e = _engine(weights_seed0, lanes=128, seed=21, ply=2, k_top=4)
+    hdrs, recs = _collect(e, 200)
+    assert _check_transitions(weights_seed0, hdrs, recs, 2) > 1000
+    # chosen action is one of the top-4 by 1-ply V whenever >= 4 moves exist
+    for hdr, d in zip(hdrs, recs):
+        for k in range(len(d["action"])):
+            cnt = int(d["n_moves"][k])
+            if cnt < 4:
+                continue
+            _, res, _ = orc.movegen(d["before"][k], int(d["mover"][k]), *d["dice"][k])
+            res = res[:500]
+            v = orc.value(weights_seed0, orc.encode_many(res, [int(d["mover"][k])] * len(res)))
+            top4 = np.argsort(-v, kind="stable")[:4]
+            assert int(d["action"][k]) in set(top4.tolist())
+    e.close()
+
+
+def test_two_ply_exact_mode_vs_reference(weights_seed0, weights_ckpt):
+    from bgx import ops
+    t = golden("two_ply.npz")
+    for w, key in ((weights_seed0, "w_seed0"), (weights_ckpt, "w_ckpt")):
+        net = ops.Net(w)
+        W = net.two_ply(torch.from_numpy(t["boards"]).cuda(), torch.from_numpy(t["opponent"]).cuda())
+        np.testing.assert_allclose(W.cpu().numpy(), t[key], atol=V_TOL, rtol=0)
