@@ -1,0 +1,61 @@
+"""World-size-2 gloo rehearsal of the multi-GPU path (bgx.dist) on CPU:
+weight broadcast from the trainer rank and the episode gather."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    from bgx import dist as bdist
+    from bgx.engine import Harvest
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(rank)
+    w = {"W1": rng.standard_normal((128, 198)).astype(np.float32), "b1": np.full(128, rank, np.float32),
+         "w2": np.ones(128, np.float32), "b2": np.array([rank], np.float32)}
+    got = bdist.broadcast_weights(w, src=0)
+    base, n = bdist.lane_block(rank, 4096)
+    # rank r finished r+1 episodes with 3*(r+1) records, tagged with its lane block
+    hdr = torch.zeros((rank + 1, 8), dtype=torch.int32)
+    hdr[:, 0] = base
+    rec = torch.full((3 * (rank + 1), 24), rank + 7, dtype=torch.int32)
+    res = bdist.gather_episodes(Harvest(hdr, rec), dst=0, keep=True)
+    if rank == 0:
+        out.put(("w", got["b1"][0], got["b2"][0]))
+        out.put(("tot", res[0], res[1], [int(p[0][0, 0]) for p in res[2]], [int(p[1][0, 0]) for p in res[2]]))
+    else:
+        out.put(("w1", got["b1"][0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_broadcast_and_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=120) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    d = {m[0]: m[1:] for m in msgs}
+    assert d["w"] == (0.0, 0.0) and d["w1"] == (0.0,)   # every rank holds rank 0's weights
+    tot_eps, tot_recs, lane0, tag = d["tot"]
+    assert (tot_eps, tot_recs) == (1 + 2, 3 + 6)
+    assert lane0 == [0, 4096] and tag == [7, 8]
