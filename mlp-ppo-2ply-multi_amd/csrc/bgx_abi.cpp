@@ -326,6 +326,7 @@ int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_op
         b.out_packed = reply;
         b.flat_count = ctr;
         b.flat_cap = cap;
+        b.flat_chunk = 256;
         b.job_off = off;
         b.job_cnt = cnt;
         b.ovf_count = ctr + 2;
@@ -343,6 +344,7 @@ int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_op
         m.rows = reply;
         m.n_rows = 0;
         m.n_rows_dev = ctr;
+        m.n_max = cap;
         m.out = V;
         m.wfrag = net->wfrag;
         m.rowc = net->rowc;
@@ -385,7 +387,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
                   e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
                   e->d_offs, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
-                  e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
+                  e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->d.action};
     for (void* p : ps) hipFree(p);
     for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
     bgx_net_destroy(e->net);
@@ -419,6 +421,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     ALLOC(e->ctr, 16);
     ALLOC(e->stats, 8);
     ALLOC(d.player, L);
+    ALLOC(d.action, L);
     ALLOC(d.dice, 2 * L);
     ALLOC(d.step, L);
     ALLOC(d.flags, L);
@@ -437,7 +440,10 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     if (cfg->ply == 2) {
         e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
         const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
-        e->reply_cap = L * per_lane;
+        int n_cu = 256;
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) n_cu = 256;
+        // + the slack of one partly used 512-row reservation per resident movegen wave
+        e->reply_cap = L * per_lane + n_cu * 10 * 512;
         ALLOC(e->sel, 4 * L);
         ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
         ALLOC(e->reply_V, e->reply_cap);
@@ -560,6 +566,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
         m.rows = e->rows;
         m.n_rows = L;
         m.n_rows_dev = e->ctr + 0;
+        m.n_max = L + e->cand_cap;
         m.out = e->V;
         m.wfrag = e->net->wfrag;
         m.rowc = e->net->rowc;
@@ -580,6 +587,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
                 b.n_jobs = 0;
                 b.n_jobs_dev = e->ctr + 0;
                 b.jobs_per_dev_unit = 21;
+                b.n_jobs_max = e->jobs_cap;
                 b.in_rows = nullptr;
                 b.in_row_base = L;
             }
@@ -587,6 +595,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
             b.out_packed = e->reply_rows;
             b.flat_count = e->ctr + 1;
             b.flat_cap = e->reply_cap;
+            b.flat_chunk = 512;
             b.job_off = e->job_off;
             b.job_cnt = e->job_cnt;
             mg_common(e, b);
@@ -597,6 +606,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
             r.rows = e->reply_rows;
             r.n_rows = 0;
             r.n_rows_dev = e->ctr + 1;
+            r.n_max = e->reply_cap;
             r.out = e->reply_V;
             r.wfrag = e->net->wfrag;
             r.rowc = e->net->rowc;
@@ -612,6 +622,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
                                         e->job_val, s));
             }
         }
+        HIP_TRY(bgx_launch_select(&e->d, s));
         HIP_TRY(bgx_launch_engine_step(&e->d, s));
     }
     return BGX_OK;

@@ -165,79 +165,15 @@ __global__ __launch_bounds__(256) void engine_step_kernel(EngineDev e) {
         int d0 = e.dice[2 * i], d1 = e.dice[2 * i + 1];
         bool done = false;
         int win_type = 0, winner = -1;
-        if (n == 0) {
+        if (n == 0 || e.action[i] < 0) {
             // pass (backgammon_env.py:139-151): no experience is recorded (worker.py:106-113)
             p ^= 1;
             rng.roll(d0, d1);
         } else {
             decided = 1;
             flags |= 16u << p;
-            const float T = e.temperature;
-            int a = -1;
-            const u32x4 ur = rng.next();
-            const float u = unit_from(ur.x);
-            if (e.ply == 2 && e.k_top == 0) {
-                // 2-ply over every candidate: score_k = alpha*V_k - beta*W_k, softmax(score/T)
-                float mx = -INFINITY;
-                for (int k = 0; k < n; ++k) {
-                    double W = 0.0;
-                    const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
-                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
-                    mx = fmaxf(mx, (float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T);
-                }
-                float sum = 0.0f;
-                for (int k = 0; k < n; ++k) {
-                    double W = 0.0;
-                    const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
-                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
-                    sum += __expf((float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T - mx);
-                }
-                const float t = u * sum;
-                float cum = 0.0f;
-                a = n - 1;
-                for (int k = 0; k < n; ++k) {
-                    double W = 0.0;
-                    const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
-                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
-                    cum += __expf((float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T - mx);
-                    if (t < cum) { a = k; break; }
-                }
-            } else if (e.ply == 2 && e.sel[4 * i] >= 0) {
-                // compute_scores_for_boards: score = alpha * S - beta * W (two_ply.py:83-85)
-                float sc[4];
-                float mx = -INFINITY;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    double W = 0.0;
-                    const float* jv = e.job_val + (size_t)(4 * i + c) * 21;
-                    for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
-                    const float S = e.V[e.sel[4 * i + c]];
-                    sc[c] = (float)((double)e.alpha * (double)S - (double)e.beta * W) / T;
-                    mx = fmaxf(mx, sc[c]);
-                }
-                float sum = 0.0f, pr[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) { pr[c] = __expf(sc[c] - mx); sum += pr[c]; }
-                const float t = u * sum;
-                // first c with t < sum_{k<=c} pr[k] (inverse CDF)
-                float cum = 0.0f;
-                int pick = 3;
-                for (int c = 0; c < 4; ++c) { cum += pr[c]; if (t < cum) { pick = c; break; } }
-                a = e.sel[4 * i + pick] - base;
-            } else {
-                // softmax(V[1:] / T) + Categorical sample (worker.py:137-143)
-                float mx = -INFINITY;
-                for (int k = 0; k < n; ++k) mx = fmaxf(mx, e.V[base + k] / T);
-                float sum = 0.0f;
-                for (int k = 0; k < n; ++k) sum += __expf(e.V[base + k] / T - mx);
-                const float t = u * sum;
-                float cum = 0.0f;
-                a = n - 1;
-                for (int k = 0; k < n; ++k) {
-                    cum += __expf(e.V[base + k] / T - mx);
-                    if (t < cum) { a = k; break; }
-                }
-            }
+            rng.ctr++;   // the select kernel's sampling uniform
+            const int a = e.action[i];
             uint32_t nb[8];
             load_packed(e.rows + (size_t)(base + a) * 8, nb);
             const int mover = p;
@@ -318,6 +254,81 @@ __global__ __launch_bounds__(256) void engine_step_kernel(EngineDev e) {
     }
 }
 
+// Action selection, one wavefront per game lane:
+//   1-ply: softmax(V[1:] / T) + Categorical sample (worker.py:137-143);
+//   2-ply K=4: score_c = alpha*S_c - beta*W_c for the top-4 (two_ply.py:83-85,
+//     W = sum_r P(r) * top-5 mean), softmax(score/T) over the four (two_ply.py
+//     hook 153-193); fewer than four moves: 1-ply;
+//   2-ply K=all: the same score for every candidate.
+// The uniform comes from the lane's Philox stream at its current counter; the
+// step kernel advances the counter past it.
+__global__ __launch_bounds__(256) void select_kernel(EngineDev e) {
+    __shared__ float xs[4][512];
+    const int w = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + w;
+    if (i >= e.L) return;
+    const int l = lane_id();
+    const int n_full = e.cand_cnt[i];
+    const int n = n_full < e.max_legal ? n_full : e.max_legal;
+    if (n == 0) {
+        if (l == 0) e.action[i] = -1;
+        return;
+    }
+    const int base = e.L + e.cand_off[i];
+    const float T = e.temperature;
+    const bool k4 = e.ply == 2 && e.k_top == 4 && e.sel[4 * i] >= 0;
+    const int m = k4 ? 4 : n;
+    float* x = xs[w];
+    for (int k = l; k < m; k += 64) {
+        float v;
+        if (k4) {
+            double W = 0.0;
+            const float* jv = e.job_val + (size_t)(4 * i + k) * 21;
+            for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
+            v = (float)((double)e.alpha * (double)e.V[e.sel[4 * i + k]] - (double)e.beta * W) / T;
+        } else if (e.ply == 2 && e.k_top == 0) {
+            double W = 0.0;
+            const float* jv = e.job_val + (size_t)(e.cand_off[i] + k) * 21;
+            for (int r = 0; r < 21; ++r) W += (double)jv[r] * kRollProbD[r];
+            v = (float)((double)e.alpha * (double)e.V[base + k] - (double)e.beta * W) / T;
+        } else {
+            v = e.V[base + k] / T;
+        }
+        x[k] = v;
+    }
+    wave_sync();
+    float mx = -INFINITY;
+    for (int k = l; k < m; k += 64) mx = fmaxf(mx, x[k]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    float sum = 0.0f;
+    for (int k = l; k < m; k += 64) sum += __expf(x[k] - mx);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    const uint64_t key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
+    const float u = unit_from(philox(key, 0x5EED0000ull, e.rng[i]).x);
+    const float t = u * sum;
+    int pick = m - 1;
+    float carry = 0.0f;
+    for (int b = 0; b < m; b += 64) {
+        const int k = b + l;
+        float p = k < m ? __expf(x[k] - mx) : 0.0f;
+        // inclusive scan of p over the wave
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float q = __shfl_up(p, off, 64);
+            if (l >= off) p += q;
+        }
+        const uint64_t hit = ballot(k < m && t < carry + p);
+        if (hit) {
+            pick = b + __ffsll((unsigned long long)hit) - 1;
+            break;
+        }
+        carry += __shfl(p, 63, 64);
+    }
+    if (l == 0) e.action[i] = k4 ? e.sel[4 * i + pick] - base : pick;
+}
+
 // 2-ply: top-4 candidates by 1-ply V (torch.topk, sorted; ties -> lower index)
 __global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -352,9 +363,10 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    const int32_t* __restrict__ job_off,
                                                    const int32_t* __restrict__ job_cnt, int n_jobs,
                                                    const unsigned* __restrict__ n_units_dev,
-                                                   int jobs_per_unit, float* __restrict__ out) {
+                                                   int jobs_per_unit, int max_jobs, float* __restrict__ out) {
     int nj = n_jobs;
     if (n_units_dev) nj += (int)(*n_units_dev) * jobs_per_unit;
+    if (nj > max_jobs) nj = max_jobs;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nj; j += gridDim.x * blockDim.x) {
         const int c = job_cnt[j], o = job_off[j];
         float t0 = -INFINITY, t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY, t4 = -INFINITY;
@@ -412,7 +424,11 @@ extern "C" hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_engine_step(const bgx::EngineDev* e, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::engine_step_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);
+    hipLaunchKernelGGL(bgx::engine_step_kernel, dim3((e->L + 63) / 64), dim3(64), 0, stream, *e);
+    return hipGetLastError();
+}
+extern "C" hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::select_kernel, dim3((e->L + 3) / 4), dim3(256), 0, stream, *e);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream) {
@@ -426,7 +442,7 @@ extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, co
     int blocks = (max_jobs + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
-                       n_units_dev, jobs_per_unit, out);
+                       n_units_dev, jobs_per_unit, max_jobs, out);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out,

@@ -18,6 +18,7 @@ struct MovegenArgs {
     int n_jobs;                  // host job count (added to the device count below)
     const unsigned* n_jobs_dev;  // optional: device count of "units"
     int jobs_per_dev_unit;       //   ... each giving this many jobs (21 for 2-ply rows)
+    int n_jobs_max;              // > 0: clamp the job count (capacity of the per-job arrays)
     int in_mode;
     const uint8_t* in_u8;        // IN_U8: [n][52]
     const uint32_t* in_packed;   // IN_PACKED: [n][8]; IN_TWOPLY: candidate rows [*][8]
@@ -32,6 +33,8 @@ struct MovegenArgs {
     int32_t* out_count;          // [n] full record count (U8 / SLOT)
     unsigned* flat_count;        // FLAT: running row count
     int flat_cap;
+    int flat_chunk;              // FLAT: rows a wave reserves per global atomic (0 = exact per job;
+                                 //   > 0 leaves unused gap rows that downstream kernels tolerate)
     int32_t* job_off;            // FLAT: [n]
     int32_t* job_cnt;            // FLAT: [n]
     // overflow handling (doubles whose frontier outgrows the LDS slice)
@@ -50,6 +53,7 @@ struct MlpArgs {
     const uint32_t* rows;        // packed boards [n][8] (flag in w[6] bit 16)
     const unsigned* n_rows_dev;  // if non-null: row count read on device
     int n_rows;                  // else: row count
+    int n_max;                   // capacity of rows/out: the device count is clamped to it
     float* out;                  // [n] V
     const uint4* wfrag;          // [2][4][13][64] fragments (16 B each)
     const float* rowc;           // [128][4]: inv_scale, w2, b1*scale, 0
@@ -91,6 +95,7 @@ struct EngineDev {
     const int32_t* cand_cnt;     // [L] full candidate count
     const float* V;              // [L + cand rows] values
     int32_t* sel;                // [L * 4] 2-ply: candidate rows chosen by 1-ply V (or -1)
+    int32_t* action;             // [L] chosen candidate index (-1 = pass), written by select
     const float* job_val;        // [L * 4 * 21] 2-ply: top-5 mean per (candidate, roll)
     const unsigned* flat_count;  // candidate rows this step (device)
     const unsigned* reply_count; // 2-ply reply rows this step (device)
@@ -115,6 +120,7 @@ hipError_t bgx_launch_unpack(const uint32_t* packed, int n, uint8_t* out, hipStr
 hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream_t stream);
 hipError_t bgx_launch_engine_step(const bgx::EngineDev* e, hipStream_t stream);
 hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream);
+hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream);
 hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt, int n_jobs,
                            const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
                            hipStream_t stream);

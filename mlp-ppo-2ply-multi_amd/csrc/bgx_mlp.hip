@@ -79,6 +79,7 @@ __global__ __launch_bounds__(512) void mlp_kernel(MlpArgs a) {
 
     int n = a.n_rows;
     if (a.n_rows_dev) n += (int)*a.n_rows_dev;
+    if (a.n_max > 0 && n > a.n_max) n = a.n_max;
     const int tiles = (n + 31) >> 5;
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5;

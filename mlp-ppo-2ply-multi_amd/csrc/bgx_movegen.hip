@@ -5,75 +5,80 @@
 // (src/backgammon/moves/handle_move_types.py:7-221) and the per-move board
 // application of generate_all_board_features (src/environments/env_helper.py:7-91).
 //
-// One job = one (board, player, dice). One wavefront per job; four independent
-// jobs per 256-thread workgroup; all job state in that wave's LDS slice.
+// One job = one (board, player, dice); one wavefront per job (64-thread
+// workgroups, persistent grid-stride over jobs); all job state lives in a
+// 16 KB LDS slice: a 1024-slot hash table of 64-bit {key, ordinal} words and
+// two 1024-entry frontier lists.
 //
-// The reference DFS records the DISTINCT resulting boards in first-reach
-// (lexicographic path) order and keeps the maximal-length plays. The wave
-// reproduces that order level-synchronously:
-//  * non-doubles: the <=15 first sub-moves of each pass sit on lanes 0..31
-//    (pass 1 = high die first on lanes 0..15, pass 2 on 16..31); the 2-move
-//    records are enumerated in (pass, i, j) order by a wave prefix sum, then
-//    deduplicated keeping the smallest ordinal (a per-slot atomicMin in an LDS
-//    hash table keyed by the exact 128-bit result board). The pass-2 skip
-//    (generate_all_moves.py:40-50) and the singles fallback
-//    (handle_move_types.py:70-81) are applied from wave ballots.
-//  * doubles: levels 1..4 are expanded breadth-first; each level's children are
-//    generated in (parent order, move order) = DFS order and deduplicated
-//    against that level only (two nodes with the same board have identical
-//    subtrees, so keeping the first keeps every later first-reach position).
-//    A node is the sorted multiset of its step sources in travel order — an
-//    exact 20-bit key of the board for a fixed root and die. The deepest
-//    non-empty level holds the records; below depth 4 a node is a record only
-//    when its parent had exactly one move (handle_move_types.py:117-169).
-// Jobs whose doubles frontier outgrows the LDS slice are re-run by a fallback
-// launch of the same code over a global-memory workspace (exact, just slower).
+// The reference's DFS emits the DISTINCT resulting boards in first-reach
+// (lexicographic path) order and keeps the maximal-length plays. Here:
+//  * every record gets an ORDINAL = its rank in that lexicographic order
+//    (an exclusive prefix sum of per-parent move counts + the move index);
+//  * records are deduplicated by an exact integer KEY of the resulting board:
+//    LDS slot = key << 32 | ordinal, inserted with one CAS; a lane that finds
+//    its key already there lowers the ordinal with one atomicMin, so each key
+//    ends up holding its first-reach ordinal;
+//  * parents sit one per lane and expand their children one move per
+//    iteration; once a parent chunk is done, a child survives iff its ordinal
+//    is the slot's ordinal, and survivors are appended in (parent, move) order.
+// Non-doubles: lanes 0..15 = pass 1 (high die first), 16..31 = pass 2
+//   (generate_all_moves.py:23-50); key = the canonical mover delta (removed /
+//   added positions after cancelling a chained checker) + hit points.
+// Doubles: up to four levels, each deduplicated on its own (equal boards have
+//   equal subtrees, so the first copy carries every later first reach); key =
+//   the sorted multiset of step sources in travel order. The deepest level is
+//   the record set; below depth 4 a node counts only if its parent had exactly
+//   one move (handle_move_types.py:117-169).
+// A job whose level outgrows the LDS table is re-run by a fallback launch of
+// the same code on a global-memory workspace (exact, slower, rare).
 #include "bgx_device.h"
 #include "bgx_kernels.h"
 
 namespace bgx {
 
-constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+constexpr unsigned long long EMPTY64 = ~0ull;
 constexpr uint32_t KEY_EMPTY4 = 0xFFFFFu;   // four empty 5-bit fields
 constexpr uint32_t KEYMASK = 0xFFFFFu;
-
-// LDS slice per wave (uint32 words)
-constexpr int S_D = 1024;   // doubles hash slots
-constexpr int F_D = 1024;   // doubles frontier capacity
-constexpr int S_N = 512;    // non-doubles hash slots (<= 450 records)
-constexpr int WAVE_WORDS = 5 * 1024;   // tkey, tmin, fa, fb, pre  (20 KB)
+constexpr uint32_t FLAG1 = 0x80000000u;      // "parent had exactly one move"
+constexpr int S_L = 1024;                    // LDS table slots
+constexpr int F_L = 1024;                    // LDS frontier capacity
+constexpr int WAVE_BYTES = S_L * 8 + 2 * F_L * 4;   // 16 KB
+constexpr int MAXC = 15;                     // moves per node per die (<= 15 checkers)
 
 struct Mem {
-    uint32_t* tkey;   // [S]      doubles keys
-    uint32_t* tmin;   // [S]      min ordinal per slot (EMPTY = free)
-    uint32_t* fa;     // [F]
-    uint32_t* fb;     // [F]
-    uint32_t* pre;    // [F]
-    uint4* tkey4;     // [S_N]    non-doubles keys (overlays fa/fb)
-    uint32_t* surv;   // [S_N]    non-doubles survivor slots (overlays pre)
+    unsigned long long* tab;   // [S]
+    uint32_t* fa;              // [F]
+    uint32_t* fb;              // [F]
     int S, F;
 };
 
-// memory-kind dependent accessors: LDS (wavefront scope) or global (agent scope)
-template <bool G> BGX_DEV uint32_t ld(const uint32_t* p) {
+// LDS (wavefront scope) or global (agent scope) accessors
+template <bool G> BGX_DEV uint32_t ld32(const uint32_t* p) {
     if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
-template <bool G> BGX_DEV void st(uint32_t* p, uint32_t v) {
+template <bool G> BGX_DEV void st32(uint32_t* p, uint32_t v) {
     if constexpr (G) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
-template <bool G> BGX_DEV uint32_t cas(uint32_t* p, uint32_t cmp, uint32_t v) {
-    if constexpr (G) {
-        __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-    } else {
+template <bool G> BGX_DEV unsigned long long ld64(const unsigned long long* p) {
+    if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV void st64(unsigned long long* p, unsigned long long v) {
+    if constexpr (G) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV unsigned long long cas64(unsigned long long* p, unsigned long long v) {
+    unsigned long long cmp = EMPTY64;
+    if constexpr (G)
+        __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
         __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
     return cmp;
 }
-template <bool G> BGX_DEV void amin(uint32_t* p, uint32_t v) {
+template <bool G> BGX_DEV void min64(unsigned long long* p, unsigned long long v) {
     if constexpr (G) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
@@ -86,82 +91,47 @@ template <bool G> BGX_DEV void sync() {
         wave_sync();
     }
 }
-
-template <bool G> BGX_DEV void clear(uint32_t* p, int n) {
-    for (int i = lane_id(); i < n; i += 64) st<G>(p + i, EMPTY);
+template <bool G> BGX_DEV void clear_tab(const Mem& M) {
+    for (int i = lane_id(); i < M.S; i += 64) st64<G>(M.tab + i, EMPTY64);
     sync<G>();
 }
 
-BGX_DEV uint32_t hash32(uint32_t k) { return k * 0x9E3779B1u; }
-BGX_DEV uint32_t hash128(const Node& n) {
-    uint32_t h = n.m0 * 0x9E3779B1u;
-    h ^= (n.m1 + 0x7F4A7C15u) * 0x85EBCA77u;
-    h ^= (n.m2 + 0x165667B1u) * 0xC2B2AE3Du;
-    h ^= (n.x + 0x27D4EB2Fu) * 0x9E3779B1u;
-    return h ^ (h >> 15);
+BGX_DEV uint32_t hash32(uint32_t k) {
+    k ^= k >> 15;
+    k *= 0x2C1B3C6Du;
+    k ^= k >> 12;
+    k *= 0x297A2D39u;
+    return k ^ (k >> 15);
 }
 
-// Deduplicate one chunk (<= 64 records, ordinals increasing across chunks).
-// Returns true on lanes whose record is the first occurrence of its key.
+// Insert (key, ord) for active lanes; returns the slot holding each lane's key.
+// `fresh` = this lane's CAS created the slot (a key new to the table).
 template <bool G>
-BGX_DEV bool dedup_u32(const Mem& M, bool active, uint32_t key, uint32_t ord) {
+BGX_DEV uint32_t dedup_insert(const Mem& M, bool active, uint32_t key, uint32_t ord, bool& fresh) {
     const uint32_t mask = (uint32_t)M.S - 1u;
-    const int shift = 32 - __builtin_ctz((uint32_t)M.S);
-    uint32_t slot = hash32(key) >> shift;
+    uint32_t slot = hash32(key) & mask;
+    const unsigned long long v = ((unsigned long long)key << 32) | ord;
     bool pending = active;
-    uint32_t my = 0;
+    fresh = false;
     while (ballot(pending)) {
-        if (pending && ld<G>(M.tmin + slot) == EMPTY) {
-            if (cas<G>(M.tmin + slot, EMPTY, ord) == EMPTY) st<G>(M.tkey + slot, key);
-        }
-        sync<G>();
         if (pending) {
-            if (ld<G>(M.tkey + slot) == key) {
-                amin<G>(M.tmin + slot, ord);
-                my = slot;
+            const unsigned long long old = cas64<G>(M.tab + slot, v);
+            if (old == EMPTY64) {
+                pending = false;
+                fresh = true;
+            } else if ((uint32_t)(old >> 32) == key) {
+                if ((uint32_t)old > ord) min64<G>(M.tab + slot, v);
                 pending = false;
             } else {
                 slot = (slot + 1u) & mask;
             }
         }
-        sync<G>();
     }
-    return active && ld<G>(M.tmin + my) == ord;
+    return slot;
 }
 
-template <bool G>
-BGX_DEV bool dedup_128(const Mem& M, bool active, const Node& key, uint32_t ord, uint32_t& myslot) {
-    const uint32_t mask = S_N - 1u;
-    uint32_t slot = (hash128(key) >> 23) & mask;
-    bool pending = active;
-    uint32_t my = 0;
-    while (ballot(pending)) {
-        if (pending && ld<G>(M.tmin + slot) == EMPTY) {
-            if (cas<G>(M.tmin + slot, EMPTY, ord) == EMPTY) {
-                uint32_t* k = (uint32_t*)(M.tkey4 + slot);
-                st<G>(k + 0, key.m0); st<G>(k + 1, key.m1); st<G>(k + 2, key.m2); st<G>(k + 3, key.x);
-            }
-        }
-        sync<G>();
-        if (pending) {
-            const uint32_t* k = (const uint32_t*)(M.tkey4 + slot);
-            bool eq = ld<G>(k + 0) == key.m0 && ld<G>(k + 1) == key.m1 && ld<G>(k + 2) == key.m2 &&
-                      ld<G>(k + 3) == key.x;
-            if (eq) {
-                amin<G>(M.tmin + slot, ord);
-                my = slot;
-                pending = false;
-            } else {
-                slot = (slot + 1u) & mask;
-            }
-        }
-        sync<G>();
-    }
-    myslot = my;
-    return active && ld<G>(M.tmin + my) == ord;
-}
-
-// relative source (travel order): 0 = BAR, then points from the mover's start
+// ------------------------------------------------------------------ keys
+// doubles: sorted multiset of relative step sources (0 = BAR, then travel order)
 BGX_DEV uint32_t rel_of(int s, int player) {
     if (s == 24) return 0u;
     return player == 0 ? (uint32_t)(s + 1) : (uint32_t)(24 - s);
@@ -176,7 +146,7 @@ BGX_DEV uint32_t key_insert(uint32_t key, uint32_t rel) {
     bool placed = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        uint32_t f = (key >> (5 * i)) & 31u;
+        const uint32_t f = (key >> (5 * i)) & 31u;
         if (!placed && rel <= f) { out |= rel << (5 * o); ++o; placed = true; }
         if (o < 4) { out |= f << (5 * o); ++o; }
     }
@@ -186,8 +156,52 @@ BGX_DEV Node rebuild(const Root& R, uint32_t key, int d) {
     Node n = root_node(R);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        uint32_t f = (key >> (5 * i)) & 31u;
+        const uint32_t f = (key >> (5 * i)) & 31u;
         if (f != 31u) n = apply_move(R, n, abs_of(f, R.player), d);
+    }
+    return n;
+}
+
+// non-doubles: positions 0..23 points, 24 = BAR (source), 25 = OFF (dest), 31 = none
+BGX_DEV int dest_of(const Root& R, int s, int d) {
+    const int t = s == 24 ? (R.player == 0 ? d - 1 : 24 - d) : (R.player == 0 ? s + d : s - d);
+    return (t < 0 || t > 23) ? 25 : t;
+}
+BGX_DEV uint32_t sort2(uint32_t a, uint32_t b) { return a <= b ? (a | (b << 5)) : (b | (a << 5)); }
+// canonical key of the board after steps (s1->t1, hit h1) and (s2->t2, hit h2); s2 = 31: single
+BGX_DEV uint32_t nd_key(uint32_t s1, uint32_t t1, bool h1, uint32_t s2, uint32_t t2, bool h2) {
+    uint32_t r0 = s1, r1 = s2, a0 = t1, a1 = t2;
+    if (s2 != 31u) {
+        if (t1 == s2) { r1 = 31u; a0 = 31u; }        // chained checker: s1 -> t1 -> t2
+        else if (t2 == s1) { r0 = 31u; a1 = 31u; }   // s2 -> s1 -> t1
+    }
+    const uint32_t hh0 = h1 ? t1 : 31u, hh1 = h2 ? t2 : 31u;
+    return sort2(r0, r1) | (sort2(a0, a1) << 10) | (sort2(hh0, hh1) << 20);
+}
+BGX_DEV void nib_add(Node& n, int p, int delta) {
+    const uint32_t v = 1u << ((p & 7) * 4);
+    const int w = p >> 3;
+    if (delta > 0) {
+        n.m0 += w == 0 ? v : 0u; n.m1 += w == 1 ? v : 0u; n.m2 += w == 2 ? v : 0u;
+    } else {
+        n.m0 -= w == 0 ? v : 0u; n.m1 -= w == 1 ? v : 0u; n.m2 -= w == 2 ? v : 0u;
+    }
+}
+BGX_DEV Node nd_board(const Root& R, uint32_t key) {
+    Node n = root_node(R);
+    // additions first, so a removal never borrows from a neighbouring nibble
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t a = (key >> (10 + 5 * i)) & 31u, h = (key >> (20 + 5 * i)) & 31u;
+        if (a == 25u) n.x += 16u;
+        else if (a < 24u) nib_add(n, (int)a, +1);
+        if (h < 24u) n.x |= 1u << (8 + h);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t r = (key >> (5 * i)) & 31u;
+        if (r == 24u) n.x -= 1u;
+        else if (r < 24u) nib_add(n, (int)r, -1);
     }
     return n;
 }
@@ -197,49 +211,53 @@ struct JobIn { Root R; int d0, d1; bool skip; };
 
 BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
     JobIn in;
-    uint32_t w[8];
+    uint32_t w0, w1, w2, w3, w4, w5, w6;
     int player = 0;
     in.skip = false;
     if (a.in_mode == IN_U8) {
         const uint32_t* b = (const uint32_t*)(a.in_u8 + (size_t)j * 52);
-        uint32_t t[13];
-#pragma unroll
-        for (int i = 0; i < 13; ++i) t[i] = b[i];
-        player = a.in_player[j];
-        u8_to_packed(t, 0, w);
-        in.d0 = a.in_dice[2 * j];
-        in.d1 = a.in_dice[2 * j + 1];
-    } else if (a.in_mode == IN_PACKED) {
-        const uint4* p = (const uint4*)(a.in_packed + (size_t)j * 8);
-        uint4 x = p[0], y = p[1];
-        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+        w0 = pack4(b[0]) | (pack4(b[1]) << 16);
+        w1 = pack4(b[2]) | (pack4(b[3]) << 16);
+        w2 = pack4(b[4]) | (pack4(b[5]) << 16);
+        w3 = pack4(b[6]) | (pack4(b[7]) << 16);
+        w4 = pack4(b[8]) | (pack4(b[9]) << 16);
+        w5 = pack4(b[10]) | (pack4(b[11]) << 16);
+        const uint32_t t = b[12];
+        w6 = (t & 15u) | (((t >> 8) & 15u) << 4) | (((t >> 16) & 15u) << 8) | (((t >> 24) & 15u) << 12);
         player = a.in_player[j];
         in.d0 = a.in_dice[2 * j];
         in.d1 = a.in_dice[2 * j + 1];
-    } else {  // IN_TWOPLY: job = row * 21 + roll; board = candidate row; player = opponent
-        int row = j / 21, roll = j - 21 * (j / 21);
-        int src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
-        if (src < 0) {
-            in.skip = true;
-            src = 0;
+    } else {
+        int src = j;
+        if (a.in_mode == IN_TWOPLY) {
+            const int row = j / 21;
+            src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
+            if (src < 0) {
+                in.skip = true;
+                src = 0;
+            }
         }
         const uint4* p = (const uint4*)(a.in_packed + (size_t)src * 8);
-        uint4 x = p[0], y = p[1];
-        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-        player = 1 - (int)((w[6] >> 16) & 1u);
-        // DICE_ROLLS (two_ply.py:10-32): (1,1),(1,2)..(1,6),(2,2)..(6,6)
-        int a0 = 1, r = roll;
-        while (r >= 7 - a0) { r -= 7 - a0; ++a0; }
-        in.d0 = a0;
-        in.d1 = a0 + r;
+        const uint4 x = p[0], y = p[1];
+        w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w; w4 = y.x; w5 = y.y; w6 = y.z;
+        if (a.in_mode == IN_TWOPLY) {
+            // two_ply.py:93-150: the opponent of the candidate's mover replies to every roll
+            player = 1 - (int)((w6 >> 16) & 1u);
+            int a0 = 1, r = j - 21 * (j / 21);   // DICE_ROLLS order (two_ply.py:10-32)
+            while (r >= 7 - a0) { r -= 7 - a0; ++a0; }
+            in.d0 = a0;
+            in.d1 = a0 + r;
+        } else {
+            player = a.in_player[j];
+            in.d0 = a.in_dice[2 * j];
+            in.d1 = a.in_dice[2 * j + 1];
+        }
     }
-    // wave-uniform root (player chosen by selects, no dynamic register indexing)
-    uint32_t s6 = w[6];
+    const bool p2 = player != 0;
     Root& R = in.R;
-    bool p2 = player != 0;
-    R.m0 = p2 ? w[3] : w[0]; R.m1 = p2 ? w[4] : w[1]; R.m2 = p2 ? w[5] : w[2];
-    R.o0 = p2 ? w[0] : w[3]; R.o1 = p2 ? w[1] : w[4]; R.o2 = p2 ? w[2] : w[5];
-    uint32_t b0 = s6 & 15u, b1 = (s6 >> 4) & 15u, f0 = (s6 >> 8) & 15u, f1 = (s6 >> 12) & 15u;
+    R.m0 = p2 ? w3 : w0; R.m1 = p2 ? w4 : w1; R.m2 = p2 ? w5 : w2;
+    R.o0 = p2 ? w0 : w3; R.o1 = p2 ? w1 : w4; R.o2 = p2 ? w2 : w5;
+    const uint32_t b0 = w6 & 15u, b1 = (w6 >> 4) & 15u, f0 = (w6 >> 8) & 15u, f1 = (w6 >> 12) & 15u;
     R.bar = p2 ? b1 : b0; R.obar = p2 ? b0 : b1;
     R.off = p2 ? f1 : f0; R.ooff = p2 ? f0 : f1;
     R.block = ge2_24(R.o0, R.o1, R.o2);
@@ -248,7 +266,7 @@ BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
     return in;
 }
 
-// write one record (lane-local) at output position k of job j
+// write record k of job j (lane-local)
 BGX_DEV void emit_one(const MovegenArgs& a, int j, const Root& R, const Node& n, int k, int base) {
     uint32_t w[8];
     node_to_packed(R, n, (uint32_t)R.player, w);
@@ -259,30 +277,57 @@ BGX_DEV void emit_one(const MovegenArgs& a, int j, const Root& R, const Node& n,
         uint32_t* dst = (uint32_t*)(a.out_u8 + ((size_t)j * a.cap + k) * 52);
 #pragma unroll
         for (int i = 0; i < 13; ++i) dst[i] = o[i];
-    } else if (a.out_mode == OUT_PACKED_SLOT) {
-        if (k >= a.cap) return;
-        uint4* dst = (uint4*)(a.out_packed + ((size_t)j * a.cap + k) * 8);
-        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    } else {  // OUT_PACKED_FLAT
-        uint4* dst = (uint4*)(a.out_packed + ((size_t)base + k) * 8);
-        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        return;
     }
+    size_t row;
+    if (a.out_mode == OUT_PACKED_SLOT) {
+        if (k >= a.cap) return;
+        row = (size_t)j * a.cap + k;
+    } else {
+        row = (size_t)base + k;
+    }
+    uint4* dst = (uint4*)(a.out_packed + row * 8);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
-// reserve output space once the job's record count is known; returns base
-BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n) {
+BGX_DEV int job_count(const MovegenArgs& a) {
+    int n = a.n_jobs;
+    if (a.n_jobs_dev) n += (int)(*a.n_jobs_dev) * a.jobs_per_dev_unit;
+    if (a.n_jobs_max > 0 && n > a.n_jobs_max) n = a.n_jobs_max;
+    return n;
+}
+
+// Per-wave output reservation for OUT_PACKED_FLAT: one global atomic per
+// `flat_chunk` rows instead of one per job (a single counter hit by every job
+// of a 2-ply launch serialises at the memory side).
+struct FlatCursor { int base = 0, left = 0; };
+
+// reserve output space once the job's record count is known; returns base (-1: overflow)
+BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
     int base = 0;
     if (a.out_mode == OUT_PACKED_FLAT) {
-        if (lane_id() == 0) {
-            base = (int)atomicAdd(a.flat_count, (unsigned)n);
-            if (base + n > a.flat_cap) {
-                atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
+        if (n <= fc.left) {
+            base = fc.base;
+            fc.base += n;
+            fc.left -= n;
+        } else {
+            // chunk = min(flat_chunk, 32 rows per job this wave still has), at least n
+            const int left_jobs = (job_count(a) - j + (int)gridDim.x - 1) / (int)gridDim.x;
+            int want = 32 * left_jobs;
+            if (want > a.flat_chunk) want = a.flat_chunk;
+            const int grab = n > want ? n : want;
+            if (lane_id() == 0) base = (int)atomicAdd(a.flat_count, (unsigned)grab);
+            base = uniform(base);
+            if (base + grab > a.flat_cap) {
+                if (lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
+                fc.left = 0;
                 base = -1;
+            } else {
+                fc.base = base + n;
+                fc.left = grab - n;
             }
         }
-        base = uniform(base);
         if (lane_id() == 0) {
             a.job_off[j] = base < 0 ? 0 : base;
             a.job_cnt[j] = base < 0 ? 0 : n;
@@ -293,15 +338,82 @@ BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n) {
     return base;
 }
 
+// ------------------------------------------------------------------ expansion
+// j-th set bit (0-based) of a 24-bit mask, j < popcount(m): branch-free narrowing
+BGX_DEV int select_bit_fast(uint32_t m, int j) {
+    int base = 0;
+    int c = __popc(m & 0xFFFu);
+    if (j >= c) { j -= c; m >>= 12; base += 12; }
+    c = __popc(m & 0x3Fu);
+    if (j >= c) { j -= c; m >>= 6; base += 6; }
+    c = __popc(m & 0x7u);
+    if (j >= c) { j -= c; m >>= 3; base += 3; }
+    m = j >= 1 ? (m & (m - 1u)) : m;
+    m = j >= 2 ? (m & (m - 1u)) : m;
+    return base + __ffs(m) - 1;
+}
+
+// Expand one chunk of parents (one per lane, c = its move count, c = 0 for
+// none). Children are enumerated FLAT in (parent, move) = ordinal order, one
+// per lane: the parent is the largest lane p with exclusive-prefix <= r (six
+// shuffle steps), its move list comes over by shuffles, kfn(p, s) gives the
+// child's key. Each 64-child chunk is deduplicated in one round; survivors
+// (first occurrences) are appended to `out` in order with payload key | tag.
+// Returns false when the table or the list would overflow (fallback path).
+template <bool G, typename KeyFn>
+BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, uint32_t ord_base, KeyFn kfn,
+                         uint32_t* out, int& n_out, int& inserted, uint32_t& total) {
+    const int l = lane_id();
+    const int incl = wave_incl_scan(c);
+    const int excl = incl - c;
+    const int T = __shfl(incl, 63, 64);
+    total = (uint32_t)T;
+    for (int b = 0; b < T; b += 64) {
+        const int r = b + l;
+        const bool act = r < T;
+        int p = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+            const int q = p + step;
+            const int e = __shfl(excl, q & 63, 64);
+            if (q < 64 && e <= r) p = q;
+        }
+        const int j = r - __shfl(excl, p, 64);
+        const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+        const int nsrc = __shfl(pm.nsrc, p, 64);
+        const int e0 = __shfl(pm.e0, p, 64), e1 = __shfl(pm.e1, p, 64);
+        const uint32_t tag = (uint32_t)__shfl((int)tagbit, p, 64);
+        const int s = j < nsrc ? select_bit_fast(src, j) : (j == nsrc ? e0 : e1);
+        const uint32_t key = kfn(p, s);
+        const uint32_t ord = ord_base + (uint32_t)r;
+        bool fresh;
+        const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
+        inserted += __popcll(ballot(fresh));
+        if (inserted > M.S - 128 || n_out + 64 > M.F) return false;
+        sync<G>();
+        const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
+        const uint64_t bm = ballot(sv);
+        if (sv) st32<G>(out + n_out + mask_prefix(bm), key | tag);
+        n_out += __popcll(bm);
+    }
+    sync<G>();
+    return true;
+}
+
 // ------------------------------------------------------------------ the job
-// returns the record count, or -1 when the LDS slice overflowed (doubles only)
+// returns the record count, or -1 when the slice overflowed (fallback)
 template <bool G>
-BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M) {
+BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc) {
     const Root& R = in.R;
     const int l = lane_id();
     const Node root = root_node(R);
+    int inserted = 0;
+    uint32_t* fin = M.fa;   // final record list
+    int nfin = 0;
+    const bool dbl = in.d0 == in.d1;
+    const int d = in.d0;
 
-    if (in.d0 != in.d1) {
+    if (!dbl) {
         // ------------------------------------------------ non-doubles
         const int H = in.d0 > in.d1 ? in.d0 : in.d1, L = in.d0 > in.d1 ? in.d1 : in.d0;
         const uint32_t okH = ok_mask(R.block, H, R.player), okL = ok_mask(R.block, L, R.player);
@@ -309,184 +421,140 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M) 
         const int pass = (l >> 4) & 1, k = l & 15;
         const bool in32 = l < 32;
         const int dA = pass ? L : H, dB = pass ? H : L;
-        const uint32_t okB = pass ? okH : okL;
         const bool v1 = in32 && k < (pass ? mL.n : mH.n);
-        Node child = root;
-        int c = 0;
-        if (v1) {
-            child = apply_move(R, root, move_source(pass ? mL : mH, k), dA);
-            c = node_moves(R, child, dB, okB).n;
-        }
+        Moves mA;
+        mA.src = pass ? mL.src : mH.src;
+        mA.nsrc = pass ? mL.nsrc : mH.nsrc;
+        mA.e0 = pass ? mL.e0 : mH.e0;
+        mA.e1 = pass ? mL.e1 : mH.e1;
+        mA.n = pass ? mL.n : mH.n;
+        int s1 = 0;
+        if (v1) s1 = move_source(mA, k);
+        const Node child = v1 ? apply_move(R, root, s1, dA) : root;
+        const Moves m2 = node_moves(R, child, dB, pass ? okH : okL);
+        const int c = v1 ? m2.n : 0;
         const bool two1 = ballot(in32 && pass == 0 && c > 0) != 0ull;
         const bool two2 = ballot(in32 && pass == 1 && c > 0) != 0ull;
         const int nH = mH.n, nL = mL.n;
-        clear<G>(M.tmin, S_N);
-        int nsurv = 0;
+        clear_tab<G>(M);
+        const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
+        const bool h1 = v1 && t1 < 24u && ((R.blot >> t1) & 1u);
         if (two1 || (nH != 1 && two2)) {
             // 2-move records in (pass, i, j) order (handle_non_doubles 43-68, both passes)
             const int cc = in32 ? c : 0;
-            const int incl = wave_incl_scan(cc);
-            const int excl = incl - cc;
-            const int T = __shfl(incl, 63, 64);
-            for (int b = 0; b < T; b += 64) {
-                const int r = b + l;
-                const bool act = r < T;
-                int p = 0;
-#pragma unroll
-                for (int step = 16; step >= 1; step >>= 1) {
-                    int q = p + step;
-                    int e = __shfl(excl, q & 31, 64);
-                    if (q < 32 && e <= r) p = q;
-                }
-                const int ep = __shfl(excl, p, 64);
-                Node ch = root;
-                if (act) {
-                    const int ppass = p >> 4, pk = p & 15;
-                    const int pA = ppass ? L : H, pB = ppass ? H : L;
-                    const Node pc = apply_move(R, root, move_source(ppass ? mL : mH, pk), pA);
-                    const Moves pm = node_moves(R, pc, pB, ppass ? okH : okL);
-                    ch = apply_move(R, pc, move_source(pm, r - ep), pB);
-                }
-                uint32_t slot;
-                const bool sv = dedup_128<G>(M, act, ch, (uint32_t)r, slot);
-                const uint64_t bm = ballot(sv);
-                if (sv) st<G>(M.surv + nsurv + mask_prefix(bm), slot);
-                nsurv += __popcll(bm);
-                sync<G>();
-            }
+            const uint32_t blot2 = R.blot & ~(h1 ? (1u << t1) : 0u);
+            auto kfn = [&](int p, int s2) -> uint32_t {
+                const uint32_t ps1 = (uint32_t)__shfl(s1, p, 64);
+                const uint32_t pt1 = (uint32_t)__shfl((int)t1, p, 64);
+                const uint32_t pb2 = (uint32_t)__shfl((int)blot2, p, 64);
+                const bool ph1 = __shfl((int)h1, p, 64) != 0;
+                const int pdB = (p >> 4) ? H : L;
+                const uint32_t t2 = (uint32_t)dest_of(R, s2, pdB);
+                const bool h2 = t2 < 24u && ((pb2 >> t2) & 1u);
+                return nd_key(ps1, pt1, ph1, (uint32_t)s2, t2, h2);
+            };
+            uint32_t tot;
+            if (!expand_flat<G>(M, m2, cc, 0u, 0u, kfn, fin, nfin, inserted, tot)) return -1;
         } else {
-            // singles: high-die singles, then (unless skipped) low-die singles
+            // singles: high-die singles, then (unless pass 2 is skipped) low-die singles
             // (handle_non_doubles 70-81; generate_all_moves.py:40-50)
             const int nL2 = (nH == 1) ? 0 : nL;
             const bool act = v1 && (pass == 0 || k < nL2);
             const uint32_t ord = pass == 0 ? (uint32_t)k : (uint32_t)(nH + k);
-            uint32_t slot;
-            const bool sv = dedup_128<G>(M, act, child, ord, slot);
+            const uint32_t key = nd_key((uint32_t)s1, t1, h1, 31u, 31u, false);
+            bool fresh;
+            const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
+            sync<G>();
+            const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
             const uint64_t bm = ballot(sv);
-            if (sv) st<G>(M.surv + mask_prefix(bm), slot);
-            nsurv = __popcll(bm);
+            if (sv) st32<G>(fin + mask_prefix(bm), key);
+            nfin = __popcll(bm);
             sync<G>();
         }
-        const int base = begin_emit(a, j, nsurv);
-        if (base < 0) return nsurv;
-        for (int b = 0; b < nsurv; b += 64) {
-            const int i = b + l;
-            if (i < nsurv) {
-                const uint32_t* kk = (const uint32_t*)(M.tkey4 + ld<G>(M.surv + i));
-                Node n = {ld<G>(kk), ld<G>(kk + 1), ld<G>(kk + 2), ld<G>(kk + 3)};
-                emit_one(a, j, R, n, i, base);
-            }
-        }
-        return nsurv;
-    }
-
-    // ---------------------------------------------------- doubles
-    const int d = in.d0;
-    const uint32_t okd = ok_mask(R.block, d, R.player);
-    uint32_t* fa = M.fa;
-    uint32_t* fb = M.fb;
-    if (l == 0) st<G>(fa, KEY_EMPTY4);
-    sync<G>();
-    int n = 1, level = 0;
-    while (level < 4) {
-        // children per frontier node -> exclusive prefix in pre[]
-        int T = 0;
-        for (int b = 0; b < n; b += 64) {
-            const int i = b + l;
-            int c = 0;
-            if (i < n) c = node_moves(R, rebuild(R, ld<G>(fa + i) & KEYMASK, d), d, okd).n;
-            const int incl = wave_incl_scan(c);
-            if (i < n) st<G>(M.pre + i, (uint32_t)(T + incl - c));
-            T += __shfl(incl, 63, 64);
-        }
+    } else {
+        // ------------------------------------------------ doubles
+        const uint32_t okd = ok_mask(R.block, d, R.player);
+        uint32_t* fa = M.fa;
+        uint32_t* fb = M.fb;
+        if (l == 0) st32<G>(fa, KEY_EMPTY4);
         sync<G>();
-        if (T == 0) break;
-        clear<G>(M.tmin, M.S);
-        int nn = 0;
-        for (int b = 0; b < T; b += 64) {
-            if (nn + 64 > M.S - 1) return -1;   // LDS slice too small: fallback
-            const int r = b + l;
-            const bool act = r < T;
-            uint32_t key = 0;
-            bool flag = false;
-            if (act) {
-                // parent = largest p with pre[p] <= r
-                int lo = 0, hi = n - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if ((int)ld<G>(M.pre + mid) <= r) lo = mid; else hi = mid - 1;
-                }
-                const uint32_t pkey = ld<G>(fa + lo) & KEYMASK;
+        int n = 1, level = 0;
+        while (level < 4) {
+            clear_tab<G>(M);
+            inserted = 0;
+            int nn = 0;
+            uint32_t T = 0;
+            for (int b = 0; b < n; b += 64) {
+                const int i = b + l;
+                const bool live = i < n;
+                const uint32_t pkey = live ? ld32<G>(fa + i) & KEYMASK : KEY_EMPTY4;
                 const Moves pm = node_moves(R, rebuild(R, pkey, d), d, okd);
-                const int s = move_source(pm, r - (int)ld<G>(M.pre + lo));
-                key = key_insert(pkey, rel_of(s, R.player));
-                flag = pm.n == 1;
+                const int cnt = live ? pm.n : 0;
+                auto kfn = [&](int p, int s) -> uint32_t {
+                    return key_insert((uint32_t)__shfl((int)pkey, p, 64), rel_of(s, R.player));
+                };
+                uint32_t tot;
+                if (!expand_flat<G>(M, pm, cnt, pm.n == 1 ? FLAG1 : 0u, T, kfn, fb, nn, inserted, tot)) return -1;
+                T += tot;
             }
-            const bool sv = dedup_u32<G>(M, act, key, (uint32_t)r);
-            const uint64_t bm = ballot(sv);
-            if (sv) st<G>(fb + nn + mask_prefix(bm), key | (flag ? 0x80000000u : 0u));
-            nn += __popcll(bm);
-            sync<G>();
+            if (T == 0) break;
+            uint32_t* t = fa; fa = fb; fb = t;
+            n = nn;
+            ++level;
         }
-        uint32_t* t = fa; fa = fb; fb = t;
-        n = nn;
-        ++level;
-    }
-    // records: the deepest level; below depth 4 only nodes whose parent had one move
-    int total = 0;
-    if (level > 0) {
-        for (int b = 0; b < n; b += 64) {
-            const int i = b + l;
-            const bool rec = i < n && (level == 4 || (ld<G>(fa + i) & 0x80000000u));
-            total += __popcll(ballot(rec));
+        // records: the deepest level; below depth 4 only nodes whose parent had one move
+        fin = fa;
+        if (level == 0) {
+            nfin = 0;
+        } else if (level == 4) {
+            nfin = n;
+        } else {
+            for (int b = 0; b < n; b += 64) {   // compact flagged nodes in place (order kept)
+                const int i = b + l;
+                const uint32_t e = i < n ? ld32<G>(fa + i) : 0u;
+                const bool rec = i < n && (e & FLAG1);
+                const uint64_t bm = ballot(rec);
+                sync<G>();
+                if (rec) st32<G>(fa + nfin + mask_prefix(bm), e);
+                nfin += __popcll(bm);
+                sync<G>();
+            }
         }
     }
-    const int base = begin_emit(a, j, total);
-    if (base < 0 || level == 0) return total;
-    int o = 0;
-    for (int b = 0; b < n; b += 64) {
+    const int base = begin_emit(a, j, nfin, fc);
+    if (base < 0) return nfin;
+    for (int b = 0; b < nfin; b += 64) {
         const int i = b + l;
-        const uint32_t e = i < n ? ld<G>(fa + i) : 0u;
-        const bool rec = i < n && (level == 4 || (e & 0x80000000u));
-        const uint64_t bm = ballot(rec);
-        if (rec) emit_one(a, j, R, rebuild(R, e & KEYMASK, d), o + mask_prefix(bm), base);
-        o += __popcll(bm);
+        if (i < nfin) {
+            const uint32_t e = ld32<G>(fin + i);
+            const Node n = dbl ? rebuild(R, e & KEYMASK, d) : nd_board(R, e);
+            emit_one(a, j, R, n, i, base);
+        }
     }
-    return total;
+    return nfin;
 }
 
 // ------------------------------------------------------------------ kernels
-BGX_DEV int job_count(const MovegenArgs& a) {
-    int n = a.n_jobs;
-    if (a.n_jobs_dev) n += (int)(*a.n_jobs_dev) * a.jobs_per_dev_unit;
-    return n;
-}
-
-// Persistent: each wave walks jobs j = wave_id, wave_id + total_waves, ...
-__global__ __launch_bounds__(256) void movegen_lds_kernel(MovegenArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t smem[4 * WAVE_WORDS];
-    const int wave = threadIdx.x >> 6;
-    uint32_t* base = smem + wave * WAVE_WORDS;
+// Persistent: wave w walks jobs w, w + gridDim.x, ...
+__global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[WAVE_BYTES / 8];
     Mem M;
-    M.tkey = base;
-    M.tmin = base + 1024;
-    M.fa = base + 2048;
-    M.fb = base + 3072;
-    M.pre = base + 4096;
-    M.tkey4 = (uint4*)(base + 2048);   // 512 x 16 B = fa + fb
-    M.surv = base + 4096;
-    M.S = S_D;
-    M.F = F_D;
+    M.tab = smem;
+    M.fa = (uint32_t*)(smem + S_L);
+    M.fb = M.fa + F_L;
+    M.S = S_L;
+    M.F = F_L;
     const int n_jobs = uniform(job_count(a));
-    for (int j = uniform((int)blockIdx.x * 4 + wave); j < n_jobs; j += (int)gridDim.x * 4) {
+    FlatCursor fc;
+    for (int j = (int)blockIdx.x; j < n_jobs; j += (int)gridDim.x) {
         const JobIn in = fetch_job(a, j);
         if (in.skip) {
-            begin_emit(a, j, 0);
+            begin_emit(a, j, 0, fc);
             continue;
         }
-        const int r = run_job<false>(a, j, in, M);
+        const int r = run_job<false>(a, j, in, M, fc);
         if (r < 0 && lane_id() == 0) {
-            unsigned slot = atomicAdd(a.ovf_count, 1u);
+            const unsigned slot = atomicAdd(a.ovf_count, 1u);
             if ((int)slot < a.ovf_cap) a.ovf_list[slot] = j;
             else atomicOr(a.err_flags, BGX_ERRF_OVF_LIST);
         }
@@ -497,22 +565,20 @@ __global__ __launch_bounds__(256) void movegen_lds_kernel(MovegenArgs a) {
 __global__ __launch_bounds__(64) void movegen_global_kernel(MovegenArgs a) {
     const int n = (int)__hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int cnt = n < a.ovf_cap ? n : a.ovf_cap;
+    if ((int)blockIdx.x >= cnt) return;
     uint32_t* base = a.ws_global + (size_t)blockIdx.x * a.ws_words_per_wave;
     Mem M;
     const int S = a.ws_slots;
-    M.tkey = base;
-    M.tmin = base + S;
+    M.tab = (unsigned long long*)base;
     M.fa = base + 2 * S;
     M.fb = base + 3 * S;
-    M.pre = base + 4 * S;
-    M.tkey4 = (uint4*)(base + 2 * S);
-    M.surv = base + 4 * S;
     M.S = S;
     M.F = S;
+    FlatCursor fc;
     for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
         const int j = uniform(a.ovf_list[t]);
         const JobIn in = fetch_job(a, j);
-        const int r = run_job<true>(a, j, in, M);
+        const int r = run_job<true>(a, j, in, M, fc);
         if (r < 0 && lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
     }
 }
@@ -523,21 +589,18 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     static int n_cu = 0;
     if (!n_cu) {
         int dev = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (n_cu <= 0) n_cu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
     }
     bgx::MovegenArgs a = *args;
     if (a.n_jobs <= 0 && !a.n_jobs_dev) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.ovf_count, 0, sizeof(unsigned), stream);
     if (e != hipSuccess) return e;
-    // persistent grid: at most 2 resident 4-wave blocks per CU (80 KB LDS each), x4 rounds
-    int blocks = n_cu * 8;
-    if (!a.n_jobs_dev) {
-        const int need = (a.n_jobs + 3) / 4;
-        if (need < blocks) blocks = need;
-    }
-    hipLaunchKernelGGL(bgx::movegen_lds_kernel, dim3(blocks), dim3(256), 0, stream, a);
+    // persistent grid: LDS admits 10 one-wave blocks (16 KB each) per CU
+    int blocks = n_cu * 10;
+    if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
+    hipLaunchKernelGGL(bgx::movegen_lds_kernel, dim3(blocks), dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(bgx::movegen_global_kernel, dim3(a.ws_waves), dim3(64), 0, stream, a);
