@@ -41,14 +41,25 @@ def load_weights():
     return {k: d[k] for k in ("W1", "b1", "w2", "b2")}
 
 
+BACKEND = os.environ.get("BGX_DIST_BACKEND", "nccl")   # "gloo": rehearsal with ranks sharing GPUs
+
+
+def _coll_device():
+    return torch.device("cuda", torch.cuda.current_device()) if BACKEND == "nccl" else torch.device("cpu")
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(BACKEND)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -66,7 +77,7 @@ def max_over_ranks(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -75,7 +86,7 @@ def sum_over_ranks(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
