@@ -54,42 +54,38 @@ struct bgx_net {
     float* w2 = nullptr;
     float b2 = 0.0f;
     uint4* wfrag = nullptr;   // split-fp16 MFMA fragments
-    float* rowc = nullptr;    // [128][4]: 2^-e, w2, b1, 0
+    float* rowc = nullptr;    // [128] w2
+    float acc_to_exp2 = 0.0f; // -2^-e log2(e)
     uint32_t* scratch = nullptr;   // packed boards for bgx_value_boards
     int scratch_n = 0;
 };
 
-// Split-fp16 fragments (see bgx_mlp.hip header for the scheme).
-static void build_fragments(const float* W1, const float* b1, const float* w2,
-                            std::vector<uint16_t>& frag, std::vector<float>& rowc) {
-    std::vector<double> Wp(128 * 198);
-    for (int j = 0; j < 128; ++j)
+// Split-fp16 fragments (see bgx_mlp.hip header for the scheme). Returns e.
+static int build_fragments(const float* W1, const float* b1, std::vector<uint16_t>& frag) {
+    std::vector<double> Wp(128 * 208, 0.0);
+    double mx = 0.0;
+    for (int j = 0; j < 128; ++j) {
         for (int k = 0; k < 198; ++k) {
             double v = W1[j * 198 + k];
             if (k == 193 || k == 195) v /= 15.0;   // feature = integer borne-off count
-            Wp[j * 198 + k] = v;
+            Wp[j * 208 + k] = v;
         }
+        Wp[j * 208 + 198] = b1[j];                 // bias column, constant 1.0 feature
+        for (int k = 0; k < 208; ++k) mx = std::fmax(mx, std::fabs(Wp[j * 208 + k]));
+    }
+    int e = 0;
+    if (mx > 0.0) {
+        e = 14 - (int)std::floor(std::log2(mx));
+        if (e > 100) e = 100;
+        if (e < -100) e = -100;
+    }
+    const double sc = std::ldexp(1.0, e);
     std::vector<_Float16> hi(128 * 208), lo(128 * 208);
-    rowc.assign(128 * 4, 0.0f);
-    for (int j = 0; j < 128; ++j) {
-        double mx = 0.0;
-        for (int k = 0; k < 198; ++k) mx = std::fmax(mx, std::fabs(Wp[j * 198 + k]));
-        int e = 0;
-        if (mx > 0.0) {
-            e = 14 - (int)std::floor(std::log2(mx));
-            if (e > 100) e = 100;
-            if (e < -100) e = -100;
-        }
-        const double sc = std::ldexp(1.0, e);
-        for (int k = 0; k < 208; ++k) {
-            const double x = k < 198 ? Wp[j * 198 + k] * sc : 0.0;
-            const _Float16 h = (_Float16)(float)x;
-            hi[j * 208 + k] = h;
-            lo[j * 208 + k] = (_Float16)(float)(x - (double)(float)h);
-        }
-        rowc[j * 4 + 0] = (float)std::ldexp(1.0, -e);
-        rowc[j * 4 + 1] = w2[j];
-        rowc[j * 4 + 2] = b1[j];
+    for (int i = 0; i < 128 * 208; ++i) {
+        const double x = Wp[i] * sc;
+        const _Float16 h = (_Float16)(float)x;
+        hi[i] = h;
+        lo[i] = (_Float16)(float)(x - (double)(float)h);
     }
     frag.assign((size_t)NFRAG * 8, 0);
     for (int t = 0; t < 2; ++t)
@@ -104,17 +100,18 @@ static void build_fragments(const float* W1, const float* b1, const float* w2,
                         std::memcpy(&bits, &v, 2);
                         frag[((((size_t)t * 4 + m) * KSTEPS + s) * 64 + l) * 8 + jj] = bits;
                     }
+    return e;
 }
 
 static int net_upload(bgx_net* n, const float* W1, const float* b1, const float* w2, const float* b2) {
     std::vector<uint16_t> frag;
-    std::vector<float> rowc;
-    build_fragments(W1, b1, w2, frag, rowc);
+    const int e = build_fragments(W1, b1, frag);
+    n->acc_to_exp2 = (float)(-std::ldexp(1.0, -e) * 1.4426950408889634);
     HIP_TRY(hipMemcpy(n->W1, W1, 128 * 198 * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(n->b1, b1, 128 * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(n->w2, w2, 128 * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(n->wfrag, frag.data(), frag.size() * 2, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(n->rowc, rowc.data(), rowc.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(n->rowc, w2, 128 * 4, hipMemcpyHostToDevice));
     n->b2 = b2[0];
     return BGX_OK;
 }
@@ -280,6 +277,7 @@ int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t
     m.wfrag = net->wfrag;
     m.rowc = net->rowc;
     m.b2 = net->b2;
+    m.acc_to_exp2 = net->acc_to_exp2;
     HIP_TRY(bgx_launch_mlp(&m, (hipStream_t)stream));
     return BGX_OK;
 }
@@ -345,10 +343,12 @@ int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_op
         m.n_rows = 0;
         m.n_rows_dev = ctr;
         m.n_max = cap;
+        m.nt = 2;
         m.out = V;
         m.wfrag = net->wfrag;
         m.rowc = net->rowc;
         m.b2 = net->b2;
+        m.acc_to_exp2 = net->acc_to_exp2;
         if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
     }
     if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, s) != hipSuccess) rc = BGX_E_HIP;
@@ -571,6 +571,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
         m.wfrag = e->net->wfrag;
         m.rowc = e->net->rowc;
         m.b2 = e->net->b2;
+        m.acc_to_exp2 = e->net->acc_to_exp2;
         if (timed(e, 1, s, true)) return BGX_E_HIP;
         HIP_TRY(bgx_launch_mlp(&m, s));
         if (timed(e, 1, s, false)) return BGX_E_HIP;
@@ -607,10 +608,12 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
             r.n_rows = 0;
             r.n_rows_dev = e->ctr + 1;
             r.n_max = e->reply_cap;
+            r.nt = 2;
             r.out = e->reply_V;
             r.wfrag = e->net->wfrag;
             r.rowc = e->net->rowc;
             r.b2 = e->net->b2;
+            r.acc_to_exp2 = e->net->acc_to_exp2;
             if (timed(e, 1, s, true)) return BGX_E_HIP;
             HIP_TRY(bgx_launch_mlp(&r, s));
             if (timed(e, 1, s, false)) return BGX_E_HIP;

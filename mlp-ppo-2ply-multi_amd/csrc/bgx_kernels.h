@@ -54,10 +54,12 @@ struct MlpArgs {
     const unsigned* n_rows_dev;  // if non-null: row count read on device
     int n_rows;                  // else: row count
     int n_max;                   // capacity of rows/out: the device count is clamped to it
+    int nt;                      // 32-board tiles per wave iteration: 1 (small batches) or 2
     float* out;                  // [n] V
     const uint4* wfrag;          // [2][4][13][64] fragments (16 B each)
-    const float* rowc;           // [128][4]: inv_scale, w2, b1*scale, 0
+    const float* rowc;           // [128] w2 (value_head.weight)
     float b2;
+    float acc_to_exp2;           // -2^-e * log2(e): accumulator -> exp2 argument of exp(-h)
 };
 
 // Self-play lane state (one engine per device), structure of arrays.
