@@ -277,15 +277,36 @@ BGX_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 // inclusive wave scan (64 lanes) of v
+// Inclusive wave scan on DPP (row_shr within 16-lane rows, then row_bcast15 /
+// row_bcast31 across rows): VALU-only, no LDS round trips.
+template <int CTRL, int ROW_MASK>
+BGX_DEV int dpp_add(int v) {
+    return v + __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, CTRL < 0x140);
+}
+template <int CTRL, int ROW_MASK>
+BGX_DEV int dpp_max(int v) {   // v >= 0
+    const int t = __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, CTRL < 0x140);
+    return v > t ? v : t;
+}
 BGX_DEV int wave_incl_scan(int v) {
-    int l = lane_id();
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int t = __shfl_up(v, off, 64);
-        if (l >= off) v += t;
-    }
+    v = dpp_add<0x111, 0xF>(v);   // row_shr:1
+    v = dpp_add<0x112, 0xF>(v);   // row_shr:2
+    v = dpp_add<0x114, 0xF>(v);   // row_shr:4
+    v = dpp_add<0x118, 0xF>(v);   // row_shr:8
+    v = dpp_add<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+    v = dpp_add<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
     return v;
 }
+BGX_DEV int wave_incl_max(int v) {   // v >= 0
+    v = dpp_max<0x111, 0xF>(v);
+    v = dpp_max<0x112, 0xF>(v);
+    v = dpp_max<0x114, 0xF>(v);
+    v = dpp_max<0x118, 0xF>(v);
+    v = dpp_max<0x142, 0xA>(v);
+    v = dpp_max<0x143, 0xC>(v);
+    return v;
+}
+BGX_DEV int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
 BGX_DEV int wave_sum(int v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

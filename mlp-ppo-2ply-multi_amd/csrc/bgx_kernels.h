@@ -45,6 +45,7 @@ struct MovegenArgs {
     int ws_waves;
     int ws_slots;                // power of two
     size_t ws_words_per_wave;    // >= 5 * ws_slots
+    int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
     unsigned* err_flags;
 };
 

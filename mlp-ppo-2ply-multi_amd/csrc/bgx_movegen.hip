@@ -6,9 +6,9 @@
 // application of generate_all_board_features (src/environments/env_helper.py:7-91).
 //
 // One job = one (board, player, dice); one wavefront per job (64-thread
-// workgroups, persistent grid-stride over jobs); all job state lives in a
-// 16 KB LDS slice: a 1024-slot hash table of 64-bit {key, ordinal} words and
-// two 1024-entry frontier lists.
+// workgroups, persistent grid-stride over jobs); all job state lives in an
+// LDS slice: a hash table of 64-bit {key, ordinal} words and two frontier
+// lists (8 KB in tier 1, see Slice below).
 //
 // The reference's DFS emits the DISTINCT resulting boards in first-reach
 // (lexicographic path) order and keeps the maximal-length plays. Here:
@@ -30,9 +30,11 @@
 //   the record set; below depth 4 a node counts only if its parent had exactly
 //   one move (handle_move_types.py:117-169).
 // A job whose level outgrows the LDS table is re-run by a fallback launch of
-// the same code on a global-memory workspace (exact, slower, rare).
+// the same code in a bigger slice, then on a global-memory workspace (exact).
 #include "bgx_device.h"
 #include "bgx_kernels.h"
+
+#include <cstdlib>
 
 namespace bgx {
 
@@ -40,15 +42,22 @@ constexpr unsigned long long EMPTY64 = ~0ull;
 constexpr uint32_t KEY_EMPTY4 = 0xFFFFFu;   // four empty 5-bit fields
 constexpr uint32_t KEYMASK = 0xFFFFFu;
 constexpr uint32_t FLAG1 = 0x80000000u;      // "parent had exactly one move"
-constexpr int S_L = 1024;                    // LDS table slots
-constexpr int F_L = 1024;                    // LDS frontier capacity
-constexpr int WAVE_BYTES = S_L * 8 + 2 * F_L * 4;   // 16 KB
-constexpr int MAXC = 15;                     // moves per node per die (<= 15 checkers)
+// LDS slices: tier 1 runs every job in SLICE_T1 bytes (512-slot table + two
+// 512-entry frontiers = 8 KB, 20 waves per CU); a job whose level outgrows it
+// is re-run by tier 2 in a 32 KB slice (2048 slots), and what still overflows
+// by the global-memory kernel. Results are identical in every tier.
+// slice = table [S] u64 | fa [S - 32] u32 | fb [S - 32] u32 | map [64] u32
+template <int S> struct Slice { static constexpr int F = S - 32, bytes = S * 8 + 2 * F * 4 + 64 * 4; };
+constexpr int S_T1 = 512;
+constexpr int S_T1L = 1024;
+constexpr int S_T2 = 2048;
+constexpr int32_t OVF_TIER3 = int32_t(0x80000000u);   // ovf_list tag: tier 2 overflowed too
 
 struct Mem {
     unsigned long long* tab;   // [S]
     uint32_t* fa;              // [F]
     uint32_t* fb;              // [F]
+    uint32_t* map;             // [64] parent start marks for one child chunk (kept zero between uses)
     int S, F;
 };
 
@@ -366,18 +375,22 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
     const int l = lane_id();
     const int incl = wave_incl_scan(c);
     const int excl = incl - c;
-    const int T = __shfl(incl, 63, 64);
+    const int T = lane63(incl);
     total = (uint32_t)T;
     for (int b = 0; b < T; b += 64) {
         const int r = b + l;
         const bool act = r < T;
-        int p = 0;
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-            const int q = p + step;
-            const int e = __shfl(excl, q & 63, 64);
-            if (q < 64 && e <= r) p = q;
-        }
+        // parent of child r: the last lane q with c > 0 and excl <= r. Parents
+        // starting inside this chunk mark map[excl - b] = q + 1; a max-scan
+        // over the marks fills the gaps; before the first mark it is q0.
+        const int st = excl - b;
+        if (c > 0 && st >= 0 && st < 64) st32<G>(M.map + st, (uint32_t)(l + 1));
+        const uint64_t cov = ballot(c > 0 && excl <= b);
+        const int q0 = cov ? 63 - __clzll((long long)cov) : 0;
+        sync<G>();
+        const int mk = wave_incl_max((int)ld32<G>(M.map + l));
+        st32<G>(M.map + l, 0u);
+        const int p = mk ? mk - 1 : q0;
         const int j = r - __shfl(excl, p, 64);
         const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
         const int nsrc = __shfl(pm.nsrc, p, 64);
@@ -389,7 +402,7 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
         bool fresh;
         const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
         inserted += __popcll(ballot(fresh));
-        if (inserted > M.S - 128 || n_out + 64 > M.F) return false;
+        if (inserted > M.S - (M.S >> 2) || n_out + 64 > M.F) return false;
         sync<G>();
         const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
         const uint64_t bm = ballot(sv);
@@ -535,15 +548,33 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
 }
 
 // ------------------------------------------------------------------ kernels
-// Persistent: wave w walks jobs w, w + gridDim.x, ...
-__global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned long long smem[WAVE_BYTES / 8];
+template <int S>
+BGX_DEV Mem lds_mem(unsigned long long* smem) {
     Mem M;
     M.tab = smem;
-    M.fa = (uint32_t*)(smem + S_L);
-    M.fb = M.fa + F_L;
-    M.S = S_L;
-    M.F = F_L;
+    M.F = Slice<S>::F;
+    M.fa = (uint32_t*)(smem + S);
+    M.fb = M.fa + M.F;
+    M.map = M.fb + M.F;
+    M.S = S;
+    M.map[lane_id()] = 0u;
+    wave_sync();
+    return M;
+}
+
+BGX_DEV void push_ovf(const MovegenArgs& a, int j) {
+    const unsigned slot = atomicAdd(a.ovf_count, 1u);
+    if ((int)slot < a.ovf_cap) a.ovf_list[slot] = j;
+    else atomicOr(a.err_flags, BGX_ERRF_OVF_LIST);
+}
+
+// Tier 1, persistent: wave w walks jobs w, w + gridDim.x, ... (S = S_T1; launches
+// with fewer jobs than resident waves use S_T1L: occupancy is moot there, and
+// a bigger table re-runs fewer jobs in tier 2)
+template <int S>
+__global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[Slice<S>::bytes / 8];
+    const Mem M = lds_mem<S>(smem);
     const int n_jobs = uniform(job_count(a));
     FlatCursor fc;
     for (int j = (int)blockIdx.x; j < n_jobs; j += (int)gridDim.x) {
@@ -552,16 +583,28 @@ __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
             begin_emit(a, j, 0, fc);
             continue;
         }
-        const int r = run_job<false>(a, j, in, M, fc);
-        if (r < 0 && lane_id() == 0) {
-            const unsigned slot = atomicAdd(a.ovf_count, 1u);
-            if ((int)slot < a.ovf_cap) a.ovf_list[slot] = j;
-            else atomicOr(a.err_flags, BGX_ERRF_OVF_LIST);
-        }
+        const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc);
+        if (r < 0 && lane_id() == 0) push_ovf(a, j);
     }
 }
 
-// Fallback for overflowed jobs: same code over a per-wave global workspace.
+// Tier 2: the jobs tier 1 listed, in a 32 KB slice; tags the ones that still overflow
+__global__ __launch_bounds__(64) void movegen_lds2_kernel(MovegenArgs a) {
+    const int n = (int)__hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int cnt = n < a.ovf_cap ? n : a.ovf_cap;
+    if ((int)blockIdx.x >= cnt) return;
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[Slice<S_T2>::bytes / 8];
+    const Mem M = lds_mem<S_T2>(smem);
+    FlatCursor fc;
+    for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
+        const int j = uniform(a.ovf_list[t]);
+        const JobIn in = fetch_job(a, j);
+        const int r = a.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M, fc);
+        if (r < 0 && lane_id() == 0) a.ovf_list[t] = j | OVF_TIER3;
+    }
+}
+
+// Tier 3: tagged jobs, same code over a per-wave global workspace.
 __global__ __launch_bounds__(64) void movegen_global_kernel(MovegenArgs a) {
     const int n = (int)__hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int cnt = n < a.ovf_cap ? n : a.ovf_cap;
@@ -572,11 +615,16 @@ __global__ __launch_bounds__(64) void movegen_global_kernel(MovegenArgs a) {
     M.tab = (unsigned long long*)base;
     M.fa = base + 2 * S;
     M.fb = base + 3 * S;
+    M.map = base + 4 * S;
     M.S = S;
     M.F = S;
+    st32<true>(M.map + lane_id(), 0u);
+    sync<true>();
     FlatCursor fc;
     for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
-        const int j = uniform(a.ovf_list[t]);
+        const int e = uniform(a.ovf_list[t]);
+        if (!(e & OVF_TIER3)) continue;
+        const int j = e & ~OVF_TIER3;
         const JobIn in = fetch_job(a, j);
         const int r = run_job<true>(a, j, in, M, fc);
         if (r < 0 && lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
@@ -597,10 +645,31 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     if (a.n_jobs <= 0 && !a.n_jobs_dev) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.ovf_count, 0, sizeof(unsigned), stream);
     if (e != hipSuccess) return e;
-    // persistent grid: LDS admits 10 one-wave blocks (16 KB each) per CU
-    int blocks = n_cu * 10;
+    // persistent grid: as many one-wave blocks as the CU admits (LDS, registers, 32 waves)
+    static int per_cu1 = 0, per_cu1l = 0, per_cu2 = 0;
+    if (!per_cu1) {
+        auto occ = [](int& n, const void* k, int dflt) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, 0) != hipSuccess || n <= 0) n = dflt;
+        };
+        occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 20);
+        occ(per_cu1l, (const void*)bgx::movegen_lds_kernel<bgx::S_T1L>, 10);
+        occ(per_cu2, (const void*)bgx::movegen_lds2_kernel, 4);
+    }
+    // test hook: route every job to tier 2 (2) or tier 3 (3)
+    if (const char* v = getenv("BGX_MG_TEST_TIER")) a.force_tier = atoi(v);
+    int t1_slots = 0;
+    if (const char* v = getenv("BGX_MG_T1_SLOTS")) t1_slots = atoi(v);
+    const bool small = !a.n_jobs_dev && a.n_jobs <= n_cu * per_cu1;
+    const bool big_tab = t1_slots ? t1_slots == bgx::S_T1L : small;
+    int blocks = n_cu * (big_tab ? per_cu1l : per_cu1);
     if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
-    hipLaunchKernelGGL(bgx::movegen_lds_kernel, dim3(blocks), dim3(64), 0, stream, a);
+    if (big_tab)
+        hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1L>, dim3(blocks), dim3(64), 0, stream, a);
+    else
+        hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(bgx::movegen_lds2_kernel, dim3(n_cu * per_cu2), dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(bgx::movegen_global_kernel, dim3(a.ws_waves), dim3(64), 0, stream, a);

@@ -41,6 +41,19 @@ def test_movegen_golden_cases(bgx_ops):
         np.testing.assert_array_equal(out[i, : o1 - o0], d["results"][o0:o1], err_msg=f"case {i}")
 
 
+@pytest.mark.parametrize("tier", ["2", "3"])
+def test_movegen_golden_cases_fallback_tiers(bgx_ops, tier, monkeypatch):
+    """Every job forced through the 32 KB LDS tier (2) or the global-memory
+    tier (3): the same ordered results as tier 1."""
+    monkeypatch.setenv("BGX_MG_TEST_TIER", tier)
+    d = golden("movegen_cases.npz")
+    out, cnt = _run_movegen(bgx_ops, d["boards"], d["player"], d["dice"], cap=1024)
+    for i in range(len(d["boards"])):
+        o0, o1 = d["offsets"][i], d["offsets"][i + 1]
+        assert cnt[i] == o1 - o0, (tier, i, cnt[i], o1 - o0)
+        np.testing.assert_array_equal(out[i, : o1 - o0], d["results"][o0:o1], err_msg=f"tier {tier} case {i}")
+
+
 def test_movegen_golden_digests(bgx_ops):
     g = golden("movegen_digests.npz")
     n = len(g["boards"])

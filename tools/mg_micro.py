@@ -56,10 +56,13 @@ def main():
     idx = rng.integers(0, len(pos), size=n)
     boards = np.stack([pos[i][0] for i in idx])
     player = np.array([pos[i][1] for i in idx], np.uint8)
+    only = sys.argv[2] if len(sys.argv) > 2 else None
     res = {}
     for name, gen in (("nondoubles", lambda: (lambda a, b: np.where(a == b, (a % 6) + 1, b))(
                           rng.integers(1, 7, n), rng.integers(1, 7, n))),
                       ("doubles", None), ("mixed21", None)):
+        if only and name != only:
+            continue
         if name == "nondoubles":
             a = rng.integers(1, 7, n)
             b = rng.integers(1, 7, n)
