@@ -91,7 +91,7 @@ def sum_over_ranks(x, world):
     return float(t.item())
 
 
-def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_every, timing):
+def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_every, timing, timing_steps=0):
     from bgx import Engine
     from bgx import dist as bdist
     w = load_weights()
@@ -117,18 +117,28 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     run(warmup)
     eng.sync()
     s0 = eng.stats()
-    if timing:
-        eng.set_timing(True)
     barrier(world)
     t0 = time.perf_counter()
-    run(steps)
+    run(steps)          # graph-launched step sequence, no events in the stream
     barrier(world)
     el = time.perf_counter() - t0
     s1 = eng.stats()
-    tm = eng.timing() if timing else None
-    eng.close()
     d = {k: s1[k] - s0[k] for k in s1}
-    return el, d, tm, gathered
+    tm = d_tm = None
+    if timing:
+        # per-kernel durations: a second pass of the same workload with HIP
+        # events recorded around every movegen / MLP launch on the engine stream
+        eng.set_timing(True)
+        t1 = time.perf_counter()
+        run(timing_steps)
+        eng.sync()
+        el_tm = time.perf_counter() - t1
+        s2 = eng.stats()
+        tm = eng.timing()
+        d_tm = {k: s2[k] - s1[k] for k in s2}
+        d_tm["elapsed_s"] = el_tm
+    eng.close()
+    return el, d, tm, d_tm, gathered
 
 
 def cpu_baseline(seconds, threads):
@@ -138,8 +148,10 @@ def cpu_baseline(seconds, threads):
     return r
 
 
-def roofline_for(d, tm, el):
-    """Dominant kernel's algorithmic rate over its average launch (HIP events)."""
+def roofline_for(d, tm):
+    """Dominant kernel's algorithmic rate over its average launch (HIP events),
+    from the timed pass `d` (stats deltas) / `tm` (event totals)."""
+    el = d["elapsed_s"]
     mg_ms, mlp_ms = tm["movegen_ms"], tm["mlp_ms"]
     out = {}
     mg_bytes = MOVEGEN_BYTES_PER_JOB * d["movegen_jobs"] + MOVEGEN_BYTES_PER_ROW * d["value_rows"]
@@ -188,20 +200,22 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
-    el, d, tm, gathered = run_engine(args, world, rank, args.ply, args.k_top, args.lanes, args.steps,
-                                     args.warmup, args.harvest_every, timing=True)
+    el, d, tm, d_tm, gathered = run_engine(args, world, rank, args.ply, args.k_top, args.lanes, args.steps,
+                                           args.warmup, args.harvest_every, timing=True,
+                                           timing_steps=min(args.steps, 200))
     el = max_over_ranks(el, world)
     total_steps = sum_over_ranks(d["env_steps"], world)
     value = total_steps / el
-    roof, kernels = roofline_for(d, tm, el)
+    roof, kernels = roofline_for(d_tm, tm)
 
     extra = {}
     if args.two_ply_steps > 0 and args.ply == 1:
-        el2, d2, tm2, _ = run_engine(args, world, rank, 2, 4, args.lanes, args.two_ply_steps, 20,
-                                     args.harvest_every, timing=True)
+        el2, d2, tm2, d2_tm, _ = run_engine(args, world, rank, 2, 4, args.lanes, args.two_ply_steps, 20,
+                                            args.harvest_every, timing=True,
+                                            timing_steps=min(args.two_ply_steps, 50))
         el2 = max_over_ranks(el2, world)
         tot2 = sum_over_ranks(d2["env_steps"], world)
-        r2, k2 = roofline_for(d2, tm2, el2)
+        r2, k2 = roofline_for(d2_tm, tm2)
         extra["two_ply_k4"] = {"value": tot2 / el2, "unit": "env_steps/s", "steps": args.two_ply_steps,
                                "ms_per_step": el2 / args.two_ply_steps * 1e3,
                                "value_rows_per_s": sum_over_ranks(d2["value_rows"], world) / el2,

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "bgx.h"
@@ -127,7 +128,7 @@ struct bgx_engine {
     float* V = nullptr;
     int32_t* cand_off = nullptr;
     int32_t* cand_cnt = nullptr;
-    unsigned* ctr = nullptr;   // [0] flat, [1] reply, [2] ovf, [3] ep, [4] err
+    unsigned* ctr = nullptr;   // [3] ep, [4] err; per-step (zeroed each step): [8] flat, [9] reply, [10] ovf, [11] ovf2
     unsigned long long* stats = nullptr;
     int32_t* sel = nullptr;
     uint32_t* reply_rows = nullptr;
@@ -150,7 +151,16 @@ struct bgx_engine {
     std::vector<int> ev_kind;
     double ms_mg = 0, ms_mlp = 0;
     int n_mg = 0, n_mlp = 0;
+    // optional hipGraph of the last n_steps sequence
+    bool use_graph = false;   // measured slower than direct launches on ROCm 7 (BGX_GRAPH=1 enables)
+    hipStream_t cap = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    int g_steps = 0;
 };
+
+namespace {
+constexpr int C_EP = 3, C_ERR = 4, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
+}
 
 extern "C" {
 
@@ -390,6 +400,8 @@ int bgx_engine_destroy(bgx_engine* e) {
                   e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->d.action};
     for (void* p : ps) hipFree(p);
     for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+    if (e->gexec) hipGraphExecDestroy(e->gexec);
+    if (e->cap) hipStreamDestroy(e->cap);
     bgx_net_destroy(e->net);
     delete e;
     return BGX_OK;
@@ -406,6 +418,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     HIP_TRY(hipSetDevice(device));
     bgx_engine* e = new bgx_engine();
     e->device = device;
+    if (const char* g = getenv("BGX_GRAPH")) e->use_graph = atoi(g) != 0;
     e->cfg = *cfg;
     const int L = cfg->lanes;
     e->cand_cap = L * (cfg->cand_per_lane > 0 ? cfg->cand_per_lane : 256);
@@ -473,19 +486,20 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     d.rows = e->rows;
     d.cand_cap = e->cand_cap;
     d.R = cfg->ring;
-    d.ep_count = e->ctr + 3;
+    d.ep_count = e->ctr + C_EP;
     d.ep_cap = ep_cap;
     d.cand_off = e->cand_off;
     d.cand_cnt = e->cand_cnt;
     d.V = e->V;
     d.sel = e->sel;
     d.job_val = e->job_val;
-    d.flat_count = e->ctr + 0;
-    d.reply_count = e->ctr + 1;
-    d.ovf_count = e->ctr + 2;
+    d.flat_count = e->ctr + C_FLAT;
+    d.reply_count = e->ctr + C_REPLY;
+    d.ovf_count = e->ctr + C_OVF;
+    d.ovf_count2 = e->ctr + C_OVF2;
     d.n_jobs2 = cfg->k_top == 4 ? L * 4 * 21 : 0;
     d.stats = e->stats;
-    d.err_flags = e->ctr + 4;
+    d.err_flags = e->ctr + C_ERR;
     if (bgx_launch_engine_reset(&d, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         bgx_engine_destroy(e);
         return fail(BGX_E_HIP, "engine reset failed");
@@ -508,19 +522,24 @@ int bgx_set_weights(bgx_engine* e, const float* h_W1, const float* h_b1, const f
         int rc = net_upload(e->net, h_W1, h_b1, h_w2, h_b2);
         if (rc) return rc;
     }
+    if (e->gexec && e->d.temperature != temperature) {
+        HIP_TRY(hipGraphExecDestroy(e->gexec));
+        e->gexec = nullptr;
+    }
     e->d.temperature = temperature;
     return BGX_OK;
 }
 
 static void mg_common(bgx_engine* e, bgx::MovegenArgs& a) {
-    a.ovf_count = e->ctr + 2;
+    a.ovf_count = e->ctr + C_OVF;
+    a.ovf_zeroed = 1;   // the per-step memset covers it
     a.ovf_list = e->ovf_list;
     a.ovf_cap = e->ovf_cap;
     a.ws_global = e->ws;
     a.ws_waves = e->ws_waves;
     a.ws_slots = e->ws_slots;
     a.ws_words_per_wave = (size_t)5 * e->ws_slots;
-    a.err_flags = e->ctr + 4;
+    a.err_flags = e->ctr + C_ERR;
 }
 
 static int timed(bgx_engine* e, int kind, hipStream_t s, bool start) {
@@ -533,18 +552,12 @@ static int timed(bgx_engine* e, int kind, hipStream_t s, bool start) {
     return BGX_OK;
 }
 
-int bgx_step(bgx_engine* e, int n_steps, void* stream) {
-    if (!e || n_steps < 0) return fail(BGX_E_ARG, "bgx_step: bad arguments");
-    if (!e->net) return fail(BGX_E_STATE, "bgx_step: bgx_set_weights first");
-    if (n_steps > e->cfg.ring - e->cfg.max_steps)
-        return fail(BGX_E_ARG, "bgx_step: n_steps=%d > ring - max_steps = %d (harvest more often)", n_steps,
-                    e->cfg.ring - e->cfg.max_steps);
-    HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = (hipStream_t)stream;
-    e->last = s;
+// the per-step launch sequence (captured into a graph by bgx_step)
+static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
     const int L = e->cfg.lanes;
     for (int it = 0; it < n_steps; ++it) {
-        HIP_TRY(hipMemsetAsync(e->ctr, 0, 8, s));   // flat + reply counters
+        // the per-step counters (flat, reply, ovf, ovf2) are zero here: engine
+        // create zeroes them and every step's last kernel resets them
         bgx::MovegenArgs a{};
         a.n_jobs = L;
         a.in_mode = bgx::IN_PACKED;
@@ -553,7 +566,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
         a.in_dice = e->d.dice;
         a.out_mode = bgx::OUT_PACKED_FLAT;
         a.out_packed = e->rows + (size_t)L * 8;
-        a.flat_count = e->ctr + 0;
+        a.flat_count = e->ctr + C_FLAT;
         a.flat_cap = e->cand_cap;
         a.job_off = e->cand_off;
         a.job_cnt = e->cand_cnt;
@@ -565,7 +578,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
         bgx::MlpArgs m{};
         m.rows = e->rows;
         m.n_rows = L;
-        m.n_rows_dev = e->ctr + 0;
+        m.n_rows_dev = e->ctr + C_FLAT;
         m.n_max = L + e->cand_cap;
         m.out = e->V;
         m.wfrag = e->net->wfrag;
@@ -586,7 +599,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
                 b.in_rows = e->sel;
             } else {
                 b.n_jobs = 0;
-                b.n_jobs_dev = e->ctr + 0;
+                b.n_jobs_dev = e->ctr + C_FLAT;
                 b.jobs_per_dev_unit = 21;
                 b.n_jobs_max = e->jobs_cap;
                 b.in_rows = nullptr;
@@ -594,19 +607,20 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
             }
             b.out_mode = bgx::OUT_PACKED_FLAT;
             b.out_packed = e->reply_rows;
-            b.flat_count = e->ctr + 1;
+            b.flat_count = e->ctr + C_REPLY;
             b.flat_cap = e->reply_cap;
             b.flat_chunk = 512;
             b.job_off = e->job_off;
             b.job_cnt = e->job_cnt;
             mg_common(e, b);
+            b.ovf_count = e->ctr + C_OVF2;
             if (timed(e, 0, s, true)) return BGX_E_HIP;
             HIP_TRY(bgx_launch_movegen(&b, s));
             if (timed(e, 0, s, false)) return BGX_E_HIP;
             bgx::MlpArgs r{};
             r.rows = e->reply_rows;
             r.n_rows = 0;
-            r.n_rows_dev = e->ctr + 1;
+            r.n_rows_dev = e->ctr + C_REPLY;
             r.n_max = e->reply_cap;
             r.nt = 2;
             r.out = e->reply_V;
@@ -621,7 +635,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
                 HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, L * 4 * 21, nullptr, 0, L * 4 * 21,
                                         e->job_val, s));
             } else {
-                HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, 0, e->ctr + 0, 21, e->jobs_cap,
+                HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, 0, e->ctr + C_FLAT, 21, e->jobs_cap,
                                         e->job_val, s));
             }
         }
@@ -631,11 +645,49 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
     return BGX_OK;
 }
 
+int bgx_step(bgx_engine* e, int n_steps, void* stream) {
+    if (!e || n_steps < 0) return fail(BGX_E_ARG, "bgx_step: bad arguments");
+    if (!e->net) return fail(BGX_E_STATE, "bgx_step: bgx_set_weights first");
+    if (n_steps > e->cfg.ring - e->cfg.max_steps)
+        return fail(BGX_E_ARG, "bgx_step: n_steps=%d > ring - max_steps = %d (harvest more often)", n_steps,
+                    e->cfg.ring - e->cfg.max_steps);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    e->last = s;
+    if (n_steps == 0) return BGX_OK;
+    // timed runs launch directly (events between the kernels); otherwise the
+    // n_steps sequence is one graph launch (kernel arguments are fixed for the
+    // engine's lifetime; bgx_set_weights drops the graph: temperature is an argument)
+    if (e->timing || !e->use_graph) return enqueue_steps(e, n_steps, s);
+    if (!e->gexec || e->g_steps != n_steps) {
+        if (e->gexec) {
+            HIP_TRY(hipGraphExecDestroy(e->gexec));
+            e->gexec = nullptr;
+        }
+        if (!e->cap) HIP_TRY(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+        HIP_TRY(hipStreamBeginCapture(e->cap, hipStreamCaptureModeRelaxed));
+        const int rc = enqueue_steps(e, n_steps, e->cap);
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(e->cap, &g);
+        if (rc) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        HIP_TRY(ec);
+        const hipError_t ei = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIP_TRY(ei);
+        e->g_steps = n_steps;
+    }
+    HIP_TRY(hipGraphLaunch(e->gexec, s));
+    return BGX_OK;
+}
+
 static int check_flags(bgx_engine* e) {
     unsigned f = 0;
-    HIP_TRY(hipMemcpy(&f, e->ctr + 4, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&f, e->ctr + C_ERR, 4, hipMemcpyDeviceToHost));
     if (f) {
-        HIP_TRY(hipMemset(e->ctr + 4, 0, 4));
+        HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
         return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
                     "workspace, 8 experience ring, 16 episode list)", f);
     }
@@ -658,7 +710,7 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
     int rc = check_flags(e);
     if (rc) return rc;
     unsigned n_eps = 0;
-    HIP_TRY(hipMemcpy(&n_eps, e->ctr + 3, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&n_eps, e->ctr + C_EP, 4, hipMemcpyDeviceToHost));
     if ((int)n_eps > e->d.ep_cap) n_eps = (unsigned)e->d.ep_cap;
     std::vector<uint32_t> hdr((size_t)n_eps * bgx::EP_WORDS);
     if (n_eps) HIP_TRY(hipMemcpy(hdr.data(), e->d.ep_list, hdr.size() * 4, hipMemcpyDeviceToHost));
@@ -680,7 +732,7 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
     }
     HIP_TRY(bgx_launch_gather(&e->d, e->d.ep_list, e->d_offs, (int)n_eps, e->out_records, s));
     HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(hipMemset(e->ctr + 3, 0, 4));
+    HIP_TRY(hipMemset(e->ctr + C_EP, 0, 4));
     out->n_episodes = (int)n_eps;
     out->n_records = total;
     out->d_headers = e->d.ep_list;

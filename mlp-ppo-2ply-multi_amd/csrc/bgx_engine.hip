@@ -250,7 +250,12 @@ __global__ __launch_bounds__(256) void engine_step_kernel(EngineDev e) {
         }
         atomicAdd(e.stats + 3, rows);
         atomicAdd(e.stats + 4, jobs);
-        atomicAdd(e.stats + 5, (unsigned long long)*e.ovf_count);
+        atomicAdd(e.stats + 5, (unsigned long long)*e.ovf_count + (e.ply == 2 ? *e.ovf_count2 : 0u));
+        // last kernel of the step: zero the per-step counters for the next one
+        *e.flat_count = 0u;
+        *e.reply_count = 0u;
+        *e.ovf_count = 0u;
+        *e.ovf_count2 = 0u;
     }
 }
 

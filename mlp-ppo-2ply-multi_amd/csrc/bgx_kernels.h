@@ -45,6 +45,7 @@ struct MovegenArgs {
     int ws_waves;
     int ws_slots;                // power of two
     size_t ws_words_per_wave;    // >= 5 * ws_slots
+    int ovf_zeroed;              // caller zeroed *ovf_count on the stream already (skip the memset)
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
     unsigned* err_flags;
 };
@@ -100,9 +101,10 @@ struct EngineDev {
     int32_t* sel;                // [L * 4] 2-ply: candidate rows chosen by 1-ply V (or -1)
     int32_t* action;             // [L] chosen candidate index (-1 = pass), written by select
     const float* job_val;        // [L * 4 * 21] 2-ply: top-5 mean per (candidate, roll)
-    const unsigned* flat_count;  // candidate rows this step (device)
-    const unsigned* reply_count; // 2-ply reply rows this step (device)
-    const unsigned* ovf_count;   // jobs sent to the fallback path this step (device)
+    unsigned* flat_count;        // candidate rows this step (device; zeroed by the step kernel)
+    unsigned* reply_count;       // 2-ply reply rows this step (device; zeroed by the step kernel)
+    unsigned* ovf_count;         // jobs sent to the fallback path this step (device)
+    unsigned* ovf_count2;        // same, for the 2-ply reply launch
     int n_jobs2;                 // 2-ply jobs this step when k_top = 4
     unsigned long long* stats;   // [8] env steps, decisions, episodes, value rows, movegen jobs, fallback
     unsigned* err_flags;

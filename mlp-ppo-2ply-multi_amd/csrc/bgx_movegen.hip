@@ -643,8 +643,11 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     }
     bgx::MovegenArgs a = *args;
     if (a.n_jobs <= 0 && !a.n_jobs_dev) return hipSuccess;
-    hipError_t e = hipMemsetAsync(a.ovf_count, 0, sizeof(unsigned), stream);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!a.ovf_zeroed) {
+        e = hipMemsetAsync(a.ovf_count, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+    }
     // persistent grid: as many one-wave blocks as the CU admits (LDS, registers, 32 waves)
     static int per_cu1 = 0, per_cu1l = 0, per_cu2 = 0;
     if (!per_cu1) {

@@ -174,3 +174,35 @@ def test_two_ply_exact_mode_vs_reference(weights_seed0, weights_ckpt):
         net = ops.Net(w)
         W = net.two_ply(torch.from_numpy(t["boards"]).cuda(), torch.from_numpy(t["opponent"]).cuda())
         np.testing.assert_allclose(W.cpu().numpy(), t[key], atol=V_TOL, rtol=0)
+
+
+def _by_episode(hdrs, recs):
+    """{(lane, episode no.): (header words 2.., {field: records})} — header
+    order is the device's atomic append order, so runs compare per episode."""
+    out = {}
+    for hdr, d in zip(hdrs, recs):
+        o = 0
+        for row in hdr:
+            n = int(row[3])
+            out[(int(row[0]), int(row[1]))] = (row[3:].copy(), {k: v[o:o + n] for k, v in d.items()})
+            o += n
+    return out
+
+
+@pytest.mark.parametrize("ply", [1, 2])
+def test_graph_launch_matches_direct_launch(ply, monkeypatch):
+    """The graph-captured step sequence (BGX_GRAPH=1) and direct launches
+    (the default) produce identical episodes and records for the same seed."""
+    w = {k: golden("weights_seed0.npz")[k] for k in ("W1", "b1", "w2", "b2")}
+    runs = []
+    for g in ("1", "0"):
+        monkeypatch.setenv("BGX_GRAPH", g)
+        e = _engine(w, lanes=256, seed=11, ply=ply, k_top=4)
+        runs.append(_by_episode(*_collect(e, 120 if ply == 1 else 40, chunk=40)))
+        e.close()
+    a, b = runs
+    assert len(a) > 0 and a.keys() == b.keys()
+    for key in a:
+        np.testing.assert_array_equal(a[key][0], b[key][0], err_msg=str(key))
+        for f in a[key][1]:
+            np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")
