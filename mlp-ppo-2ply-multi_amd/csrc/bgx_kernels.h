@@ -46,6 +46,7 @@ struct MovegenArgs {
     int ws_slots;                // power of two
     size_t ws_words_per_wave;    // >= 5 * ws_slots
     int ovf_zeroed;              // caller zeroed *ovf_count on the stream already (skip the memset)
+    int heavy_t;                 // set by the launcher: doubles level size handed to the block tier
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
     unsigned* err_flags;
 };

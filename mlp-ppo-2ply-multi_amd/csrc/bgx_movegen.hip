@@ -49,7 +49,6 @@ constexpr uint32_t FLAG1 = 0x80000000u;      // "parent had exactly one move"
 // slice = table [S] u64 | fa [S - 32] u32 | fb [S - 32] u32 | map [64] u32
 template <int S> struct Slice { static constexpr int F = S - 32, bytes = S * 8 + 2 * F * 4 + 64 * 4; };
 constexpr int S_T1 = 512;
-constexpr int S_T1L = 1024;
 constexpr int S_T2 = 2048;
 constexpr int32_t OVF_TIER3 = int32_t(0x80000000u);   // ovf_list tag: tier 2 overflowed too
 
@@ -362,6 +361,23 @@ BGX_DEV int select_bit_fast(uint32_t m, int j) {
     return base + __ffs(m) - 1;
 }
 
+// Parent lane of child r = b + lane in a flat enumeration: the last lane q
+// with c > 0 and excl <= r. Parents starting inside [b, b + 64) mark
+// map[excl - b] = q + 1; a max-scan over the marks fills the gaps; before the
+// first mark it is q0. `map` (64 words) is zero on entry and on return.
+template <bool G>
+BGX_DEV int flat_parent(uint32_t* map, int excl, int c, int b) {
+    const int l = lane_id();
+    const int st = excl - b;
+    if (c > 0 && st >= 0 && st < 64) st32<G>(map + st, (uint32_t)(l + 1));
+    const uint64_t cov = ballot(c > 0 && excl <= b);
+    const int q0 = cov ? 63 - __clzll((long long)cov) : 0;
+    sync<G>();
+    const int mk = wave_incl_max((int)ld32<G>(map + l));
+    st32<G>(map + l, 0u);
+    return mk ? mk - 1 : q0;
+}
+
 // Expand one chunk of parents (one per lane, c = its move count, c = 0 for
 // none). Children are enumerated FLAT in (parent, move) = ordinal order, one
 // per lane: the parent is the largest lane p with exclusive-prefix <= r (six
@@ -380,17 +396,7 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
     for (int b = 0; b < T; b += 64) {
         const int r = b + l;
         const bool act = r < T;
-        // parent of child r: the last lane q with c > 0 and excl <= r. Parents
-        // starting inside this chunk mark map[excl - b] = q + 1; a max-scan
-        // over the marks fills the gaps; before the first mark it is q0.
-        const int st = excl - b;
-        if (c > 0 && st >= 0 && st < 64) st32<G>(M.map + st, (uint32_t)(l + 1));
-        const uint64_t cov = ballot(c > 0 && excl <= b);
-        const int q0 = cov ? 63 - __clzll((long long)cov) : 0;
-        sync<G>();
-        const int mk = wave_incl_max((int)ld32<G>(M.map + l));
-        st32<G>(M.map + l, 0u);
-        const int p = mk ? mk - 1 : q0;
+        const int p = flat_parent<G>(M.map, excl, c, b);
         const int j = r - __shfl(excl, p, 64);
         const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
         const int nsrc = __shfl(pm.nsrc, p, 64);
@@ -415,8 +421,11 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
 
 // ------------------------------------------------------------------ the job
 // returns the record count, or -1 when the slice overflowed (fallback)
+// heavy_t: a doubles level with more children than this returns -2 (the
+// small-launch kernel then expands the job with the whole block)
 template <bool G>
-BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc) {
+BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc,
+                    int heavy_t = 0x7FFFFFFF) {
     const Root& R = in.R;
     const int l = lane_id();
     const Node root = root_node(R);
@@ -509,6 +518,7 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
                 uint32_t tot;
                 if (!expand_flat<G>(M, pm, cnt, pm.n == 1 ? FLAG1 : 0u, T, kfn, fb, nn, inserted, tot)) return -1;
                 T += tot;
+                if ((int)T > heavy_t) return -2;
             }
             if (T == 0) break;
             uint32_t* t = fa; fa = fb; fb = t;
@@ -547,6 +557,170 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
     return nfin;
 }
 
+// ------------------------------------------------------------------ block-cooperative doubles
+// Small launches (no more jobs than resident waves, e.g. the 1-ply step) are
+// bound by their slowest job: a doubles roll with hundreds of results. A
+// doubles job whose level outgrows HEAVY_T children in its wave is expanded
+// again by the whole 16-wave block, level by level:
+//  1. parents (2 per thread): rebuild, move list -> LDS (src mask, packed
+//     extras, exclusive child prefix from a block scan), and a child -> parent
+//     map (u16 per child);
+//  2. children (one per thread per round): insert key << 32 | (ordinal << 1 |
+//     parent-had-one-move) into a table sized for the level (dedup_insert's
+//     CAS / atomicMin leave each key with its first-reach ordinal);
+//  3. survivors = the occupied slots: set bit[ordinal], prefix-popcount the
+//     bitmap, and each slot writes its key to the next frontier at its rank,
+//     i.e. in first-reach order.
+constexpr int BW = 16;                // waves per block
+constexpr int NTH = 64 * BW;          // threads per block
+constexpr int K_S = 4096;             // max table slots
+constexpr int K_F = 2 * NTH;          // frontier capacity (2 parents per thread)
+constexpr int K_TMAX = 16384;         // children per level
+constexpr int HEAVY_T = 256;
+struct CoopLds {
+    unsigned long long tab[K_S];
+    uint32_t fa[K_F], fb[K_F];
+    uint32_t psrc[K_F], ppack[K_F], pexcl[K_F];
+    uint16_t map[K_TMAX];
+    uint32_t bits[K_TMAX / 32];
+    uint16_t pre[K_TMAX / 32];
+    uint32_t wsum[BW];
+    uint32_t misc[8];                 // [0] inserted [1] record count [2] emit base [3] heavy mask
+};
+constexpr int SMALL_BYTES = sizeof(CoopLds) > (size_t)BW * Slice<S_T1>::bytes ? (int)sizeof(CoopLds)
+                                                                              : BW * Slice<S_T1>::bytes;
+
+// block-wide exclusive scan of one value per thread; `total` = block sum
+BGX_DEV int block_excl_scan(CoopLds& C, int v, int& total) {
+    const int w = (int)threadIdx.x >> 6;
+    const int incl = wave_incl_scan(v);
+    if (lane_id() == 63) C.wsum[w] = (uint32_t)incl;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < BW; ++k) {
+        const int t = (int)C.wsum[k];
+        before += k < w ? t : 0;
+        total += t;
+    }
+    __syncthreads();
+    return before + incl - v;
+}
+
+// returns the record count (records in `fin`), -1 = overflow (tier 3)
+BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin) {
+    const Root& R = in.R;
+    const int d = in.d0;
+    const int t = (int)threadIdx.x, l = lane_id();
+    const uint32_t okd = ok_mask(R.block, d, R.player);
+    uint32_t* fa = C.fa;
+    uint32_t* fb = C.fb;
+    if (t == 0) fa[0] = KEY_EMPTY4;
+    __syncthreads();
+    int n = 1, level = 0;
+    while (level < 4) {
+        // 1. parents 2t, 2t + 1
+        int c[2];
+        uint32_t src[2], pack[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = 2 * t + h;
+            const uint32_t pkey = i < n ? fa[i] & KEYMASK : KEY_EMPTY4;
+            const Moves pm = node_moves(R, rebuild(R, pkey, d), d, okd);
+            c[h] = i < n ? pm.n : 0;
+            src[h] = pm.src;
+            pack[h] = (uint32_t)pm.nsrc | ((uint32_t)(pm.e0 + 1) << 5) | ((uint32_t)(pm.e1 + 1) << 10) |
+                      (pm.n == 1 ? 1u << 15 : 0u);
+        }
+        int T;
+        const int ex0 = block_excl_scan(C, c[0] + c[1], T);
+        if (T == 0) break;                      // uniform
+        if (T > K_TMAX) return -1;
+        int S = 64;
+        while (S < 2 * T && S < K_S) S <<= 1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = 2 * t + h;
+            if (i < n) {
+                const int ex = ex0 + (h ? c[0] : 0);
+                C.psrc[i] = src[h];
+                C.ppack[i] = pack[h];
+                C.pexcl[i] = (uint32_t)ex;
+                for (int k = 0; k < c[h]; ++k) C.map[ex + k] = (uint16_t)i;
+            }
+        }
+        for (int i = t; i < S; i += NTH) C.tab[i] = EMPTY64;
+        const int nwd = (T + 31) >> 5;
+        for (int i = t; i < nwd; i += NTH) C.bits[i] = 0u;
+        if (t == 0) C.misc[0] = 0u;
+        __syncthreads();
+        // 2. children
+        Mem M;
+        M.tab = C.tab;
+        M.S = S;
+        int fresh_n = 0;
+        for (int b = 0; b < T; b += NTH) {     // uniform trip count
+            const int r = b + t;
+            const bool act = r < T;
+            const int p = act ? (int)C.map[r] : 0;
+            const uint32_t pk = C.ppack[p];
+            const int jj = r - (int)C.pexcl[p];
+            const int nsrc = (int)(pk & 31u);
+            const int sx = jj < nsrc ? select_bit_fast(C.psrc[p], jj)
+                                     : (jj == nsrc ? (int)((pk >> 5) & 31u) - 1 : (int)((pk >> 10) & 31u) - 1);
+            const uint32_t key = key_insert(fa[p] & KEYMASK, rel_of(sx, R.player));
+            const uint32_t ordw = ((uint32_t)r << 1) | ((pk >> 15) & 1u);
+            bool fresh;
+            dedup_insert<false>(M, act, key, ordw, fresh);
+            fresh_n += __popcll(ballot(fresh));
+        }
+        if (l == 0 && fresh_n) atomicAdd(&C.misc[0], (uint32_t)fresh_n);
+        __syncthreads();
+        if ((int)C.misc[0] > K_F) return -1;   // uniform
+        // 3. survivors in ordinal order
+        for (int i = t; i < S; i += NTH) {
+            const unsigned long long v = C.tab[i];
+            if (v != EMPTY64) {
+                const uint32_t o = (uint32_t)v >> 1;
+                atomicOr(&C.bits[o >> 5], 1u << (o & 31));
+            }
+        }
+        __syncthreads();
+        int nn;
+        const int cw = t < nwd ? __popc(C.bits[t]) : 0;   // nwd <= K_TMAX / 32 = NTH / 2
+        const int pw = block_excl_scan(C, cw, nn);
+        if (t < nwd) C.pre[t] = (uint16_t)pw;
+        __syncthreads();
+        for (int i = t; i < S; i += NTH) {
+            const unsigned long long v = C.tab[i];
+            if (v != EMPTY64) {
+                const uint32_t ow = (uint32_t)v, o = ow >> 1;
+                const int rank = (int)C.pre[o >> 5] + __popc(C.bits[o >> 5] & ((1u << (o & 31)) - 1u));
+                fb[rank] = (uint32_t)(v >> 32) | ((ow & 1u) ? FLAG1 : 0u);
+            }
+        }
+        __syncthreads();
+        uint32_t* tmp = fa; fa = fb; fb = tmp;
+        n = nn;
+        ++level;
+    }
+    fin = fa;
+    if (level == 4) return n;
+    if (level == 0) return 0;
+    // below depth 4: only nodes whose parent had one move (order kept)
+    const int i0 = 2 * t;
+    const uint32_t e0 = i0 < n ? fa[i0] : 0u, e1 = i0 + 1 < n ? fa[i0 + 1] : 0u;
+    const int f0 = (i0 < n && (e0 & FLAG1)) ? 1 : 0, f1 = (i0 + 1 < n && (e1 & FLAG1)) ? 1 : 0;
+    int nf;
+    const int pos = block_excl_scan(C, f0 + f1, nf);
+    if (f0) fb[pos] = e0;
+    if (f1) fb[pos + f0] = e1;
+    __syncthreads();
+    fin = fb;
+    return nf;
+}
+
 // ------------------------------------------------------------------ kernels
 template <int S>
 BGX_DEV Mem lds_mem(unsigned long long* smem) {
@@ -568,9 +742,9 @@ BGX_DEV void push_ovf(const MovegenArgs& a, int j) {
     else atomicOr(a.err_flags, BGX_ERRF_OVF_LIST);
 }
 
-// Tier 1, persistent: wave w walks jobs w, w + gridDim.x, ... (S = S_T1; launches
-// with fewer jobs than resident waves use S_T1L: occupancy is moot there, and
-// a bigger table re-runs fewer jobs in tier 2)
+// Tier 1, persistent: wave w walks jobs w, w + gridDim.x, ... Launches with
+// no more jobs than resident waves (latency-bound) also hand doubles jobs with
+// a level over HEAVY_T children to tier 2, where a block expands them.
 template <int S>
 __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned long long smem[Slice<S>::bytes / 8];
@@ -583,24 +757,59 @@ __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
             begin_emit(a, j, 0, fc);
             continue;
         }
-        const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc);
-        if (r < 0 && lane_id() == 0) push_ovf(a, j);
+        const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc, a.heavy_t);
+        if (r < 0 && lane_id() == 0) push_ovf(a, j);   // overflow (-1) or heavy doubles (-2)
     }
 }
 
-// Tier 2: the jobs tier 1 listed, in a 32 KB slice; tags the ones that still overflow
-__global__ __launch_bounds__(64) void movegen_lds2_kernel(MovegenArgs a) {
+// Tier 2, one 16-wave block per listed job: doubles are expanded by the
+// whole block (coop_doubles); a non-doubles job runs in wave 0 in a 32 KB
+// slice. Jobs that still do not fit are tagged for tier 3.
+__global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
     const int n = (int)__hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int cnt = n < a.ovf_cap ? n : a.ovf_cap;
     if ((int)blockIdx.x >= cnt) return;
-    __shared__ __attribute__((aligned(16))) unsigned long long smem[Slice<S_T2>::bytes / 8];
-    const Mem M = lds_mem<S_T2>(smem);
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[sizeof(CoopLds) / 8];
+    __shared__ uint32_t emit_s;
+    CoopLds& C = *(CoopLds*)smem;
+    const int w = (int)threadIdx.x >> 6, l = lane_id();
     FlatCursor fc;
     for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
-        const int j = uniform(a.ovf_list[t]);
+        const int j = a.ovf_list[t];
+        if (j & OVF_TIER3) continue;           // uniform
         const JobIn in = fetch_job(a, j);
-        const int r = a.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M, fc);
-        if (r < 0 && lane_id() == 0) a.ovf_list[t] = j | OVF_TIER3;
+        int r;
+        if (in.d0 != in.d1) {
+            r = 0;
+            if (w == 0) {
+                static_assert(Slice<S_T2>::bytes <= sizeof(CoopLds), "slice fits");
+                const Mem M = lds_mem<S_T2>(smem);
+                r = a.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M, fc);
+                if (r < 0 && l == 0) a.ovf_list[t] = j | OVF_TIER3;
+            }
+            __syncthreads();
+            continue;
+        }
+        uint32_t* fin = nullptr;
+        const int nfin = a.force_tier >= 3 ? -1 : coop_doubles(in, C, fin);
+        if (nfin < 0) {
+            if (threadIdx.x == 0) a.ovf_list[t] = j | OVF_TIER3;
+            __syncthreads();
+            continue;
+        }
+        if (w == 0) {
+            const int base = begin_emit(a, j, nfin, fc);
+            if (l == 0) emit_s = (uint32_t)base;
+        }
+        __syncthreads();
+        const int base = (int)emit_s;
+        if (base >= 0) {
+            for (int i = (int)threadIdx.x; i < nfin; i += NTH) {
+                const uint32_t e = fin[i];
+                emit_one(a, j, in.R, rebuild(in.R, e & KEYMASK, in.d0), i, base);
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -649,30 +858,28 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         if (e != hipSuccess) return e;
     }
     // persistent grid: as many one-wave blocks as the CU admits (LDS, registers, 32 waves)
-    static int per_cu1 = 0, per_cu1l = 0, per_cu2 = 0;
+    static int per_cu1 = 0, per_cub = 0;
     if (!per_cu1) {
-        auto occ = [](int& n, const void* k, int dflt) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 64, 0) != hipSuccess || n <= 0) n = dflt;
+        auto occ = [](int& n, const void* k, int threads, int dflt) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n <= 0) n = dflt;
         };
-        occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 20);
-        occ(per_cu1l, (const void*)bgx::movegen_lds_kernel<bgx::S_T1L>, 10);
-        occ(per_cu2, (const void*)bgx::movegen_lds2_kernel, 4);
+        occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 64, 20);
+        occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
     }
     // test hook: route every job to tier 2 (2) or tier 3 (3)
     if (const char* v = getenv("BGX_MG_TEST_TIER")) a.force_tier = atoi(v);
-    int t1_slots = 0;
-    if (const char* v = getenv("BGX_MG_T1_SLOTS")) t1_slots = atoi(v);
-    const bool small = !a.n_jobs_dev && a.n_jobs <= n_cu * per_cu1;
-    const bool big_tab = t1_slots ? t1_slots == bgx::S_T1L : small;
-    int blocks = n_cu * (big_tab ? per_cu1l : per_cu1);
+    // heavy doubles go to the block-cooperative tier 2 when the launch is
+    // latency-bound (BGX_MG_COOP=1/0 forces it on/off)
+    int coop = -1;
+    if (const char* v = getenv("BGX_MG_COOP")) coop = atoi(v);
+    int blocks = n_cu * per_cu1;
+    const bool few = !a.n_jobs_dev && a.n_jobs <= blocks;
+    a.heavy_t = (coop == 1 || (coop < 0 && few)) ? bgx::HEAVY_T : 0x7FFFFFFF;
     if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
-    if (big_tab)
-        hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1L>, dim3(blocks), dim3(64), 0, stream, a);
-    else
-        hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bgx::movegen_lds2_kernel, dim3(n_cu * per_cu2), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(bgx::movegen_block_kernel, dim3(n_cu * per_cub), dim3(bgx::NTH), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(bgx::movegen_global_kernel, dim3(a.ws_waves), dim3(64), 0, stream, a);

@@ -32,7 +32,11 @@ def _run_movegen(ops, boards, player, dice, cap):
     return out.cpu().numpy(), cnt.cpu().numpy()
 
 
-def test_movegen_golden_cases(bgx_ops):
+@pytest.mark.parametrize("coop", ["0", "1"])
+def test_movegen_golden_cases(bgx_ops, coop, monkeypatch):
+    """Heavy doubles jobs expanded per wave (0) or handed to the
+    block-cooperative tier (1)."""
+    monkeypatch.setenv("BGX_MG_COOP", coop)
     d = golden("movegen_cases.npz")
     out, cnt = _run_movegen(bgx_ops, d["boards"], d["player"], d["dice"], cap=1024)
     for i in range(len(d["boards"])):
@@ -83,7 +87,9 @@ def _fuzz_positions(seed, n_games):
     return pos
 
 
-def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops):
+@pytest.mark.parametrize("coop", ["0", "1"])
+def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, coop, monkeypatch):
+    monkeypatch.setenv("BGX_MG_COOP", coop)
     pos = _fuzz_positions(1234, 40)
     rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
     boards = np.stack([p[0] for p in pos for _ in rolls])
