@@ -180,7 +180,7 @@ int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t*
     static int cur_dev = -1;
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    const int ovf_cap = 1 << 16, ws_waves = 64, ws_slots = 16384;
+    const int ovf_cap = 1 << 16, ws_waves = 256, ws_slots = 16384;
     if (!ctr || cur_dev != dev) {
         if (dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
             return BGX_E_HIP;
@@ -446,7 +446,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     ALLOC(d.ring, (size_t)L * cfg->ring * bgx::REC_WORDS);
     ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
     e->ovf_cap = 1 << 16;
-    e->ws_waves = 128;
+    e->ws_waves = 256;   // one global-memory fallback slice per tier-2 block
     e->ws_slots = 16384;
     ALLOC(e->ovf_list, e->ovf_cap);
     ALLOC(e->ws, (size_t)e->ws_waves * 5 * e->ws_slots);

@@ -50,7 +50,6 @@ constexpr uint32_t FLAG1 = 0x80000000u;      // "parent had exactly one move"
 template <int S> struct Slice { static constexpr int F = S - 32, bytes = S * 8 + 2 * F * 4 + 64 * 4; };
 constexpr int S_T1 = 512;
 constexpr int S_T2 = 2048;
-constexpr int32_t OVF_TIER3 = int32_t(0x80000000u);   // ovf_list tag: tier 2 overflowed too
 
 struct Mem {
     unsigned long long* tab;   // [S]
@@ -576,7 +575,7 @@ constexpr int NTH = 64 * BW;          // threads per block
 constexpr int K_S = 4096;             // max table slots
 constexpr int K_F = 2 * NTH;          // frontier capacity (2 parents per thread)
 constexpr int K_TMAX = 16384;         // children per level
-constexpr int HEAVY_T = 256;
+constexpr int HEAVY_T = 128;             // measured: 256 / 128 / 64 -> 128 best (1-ply)
 struct CoopLds {
     unsigned long long tab[K_S];
     uint32_t fa[K_F], fb[K_F];
@@ -587,9 +586,6 @@ struct CoopLds {
     uint32_t wsum[BW];
     uint32_t misc[8];                 // [0] inserted [1] record count [2] emit base [3] heavy mask
 };
-constexpr int SMALL_BYTES = sizeof(CoopLds) > (size_t)BW * Slice<S_T1>::bytes ? (int)sizeof(CoopLds)
-                                                                              : BW * Slice<S_T1>::bytes;
-
 // block-wide exclusive scan of one value per thread; `total` = block sum
 BGX_DEV int block_excl_scan(CoopLds& C, int v, int& total) {
     const int w = (int)threadIdx.x >> 6;
@@ -764,7 +760,8 @@ __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
 
 // Tier 2, one 16-wave block per listed job: doubles are expanded by the
 // whole block (coop_doubles); a non-doubles job runs in wave 0 in a 32 KB
-// slice. Jobs that still do not fit are tagged for tier 3.
+// slice. A job that still does not fit (tier 3) runs in wave 0 over the
+// block's global-memory workspace (same code, exact).
 __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
     const int n = (int)__hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int cnt = n < a.ovf_cap ? n : a.ovf_cap;
@@ -774,26 +771,38 @@ __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
     CoopLds& C = *(CoopLds*)smem;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
     FlatCursor fc;
+    // tier 3, wave 0 only
+    auto run_global = [&](int j, const JobIn& in) {
+        uint32_t* base = a.ws_global + (size_t)blockIdx.x * a.ws_words_per_wave;
+        Mem G;
+        const int S = a.ws_slots;
+        G.tab = (unsigned long long*)base;
+        G.fa = base + 2 * S;
+        G.fb = base + 3 * S;
+        G.map = base + 4 * S;
+        G.S = S;
+        G.F = S;
+        st32<true>(G.map + l, 0u);
+        sync<true>();
+        if (run_job<true>(a, j, in, G, fc) < 0 && l == 0) atomicOr(a.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
+    };
     for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
         const int j = a.ovf_list[t];
-        if (j & OVF_TIER3) continue;           // uniform
         const JobIn in = fetch_job(a, j);
-        int r;
-        if (in.d0 != in.d1) {
-            r = 0;
+        if (in.d0 != in.d1 || a.force_tier >= 3) {
             if (w == 0) {
                 static_assert(Slice<S_T2>::bytes <= sizeof(CoopLds), "slice fits");
                 const Mem M = lds_mem<S_T2>(smem);
-                r = a.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M, fc);
-                if (r < 0 && l == 0) a.ovf_list[t] = j | OVF_TIER3;
+                const int r = a.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M, fc);
+                if (r < 0) run_global(j, in);
             }
             __syncthreads();
             continue;
         }
         uint32_t* fin = nullptr;
-        const int nfin = a.force_tier >= 3 ? -1 : coop_doubles(in, C, fin);
+        const int nfin = coop_doubles(in, C, fin);
         if (nfin < 0) {
-            if (threadIdx.x == 0) a.ovf_list[t] = j | OVF_TIER3;
+            if (w == 0) run_global(j, in);
             __syncthreads();
             continue;
         }
@@ -810,33 +819,6 @@ __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
             }
         }
         __syncthreads();
-    }
-}
-
-// Tier 3: tagged jobs, same code over a per-wave global workspace.
-__global__ __launch_bounds__(64) void movegen_global_kernel(MovegenArgs a) {
-    const int n = (int)__hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int cnt = n < a.ovf_cap ? n : a.ovf_cap;
-    if ((int)blockIdx.x >= cnt) return;
-    uint32_t* base = a.ws_global + (size_t)blockIdx.x * a.ws_words_per_wave;
-    Mem M;
-    const int S = a.ws_slots;
-    M.tab = (unsigned long long*)base;
-    M.fa = base + 2 * S;
-    M.fb = base + 3 * S;
-    M.map = base + 4 * S;
-    M.S = S;
-    M.F = S;
-    st32<true>(M.map + lane_id(), 0u);
-    sync<true>();
-    FlatCursor fc;
-    for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
-        const int e = uniform(a.ovf_list[t]);
-        if (!(e & OVF_TIER3)) continue;
-        const int j = e & ~OVF_TIER3;
-        const JobIn in = fetch_job(a, j);
-        const int r = run_job<true>(a, j, in, M, fc);
-        if (r < 0 && lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
     }
 }
 
@@ -874,14 +856,16 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     if (const char* v = getenv("BGX_MG_COOP")) coop = atoi(v);
     int blocks = n_cu * per_cu1;
     const bool few = !a.n_jobs_dev && a.n_jobs <= blocks;
-    a.heavy_t = (coop == 1 || (coop < 0 && few)) ? bgx::HEAVY_T : 0x7FFFFFFF;
+    int heavy = bgx::HEAVY_T;
+    if (const char* v = getenv("BGX_MG_HEAVY_T")) heavy = atoi(v);
+    a.heavy_t = (coop == 1 || (coop < 0 && few)) ? heavy : 0x7FFFFFFF;
     if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
     hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bgx::movegen_block_kernel, dim3(n_cu * per_cub), dim3(bgx::NTH), 0, stream, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bgx::movegen_global_kernel, dim3(a.ws_waves), dim3(64), 0, stream, a);
+    // tier 2 (+ tier 3 in the same block): one block per CU, at most one per workspace slice
+    int bblocks = n_cu * per_cub;
+    if (bblocks > a.ws_waves) bblocks = a.ws_waves;
+    hipLaunchKernelGGL(bgx::movegen_block_kernel, dim3(bblocks), dim3(bgx::NTH), 0, stream, a);
     return hipGetLastError();
 }
