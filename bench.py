@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=7, help="mirrors src/main.py:86 (7 workers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timing-steps", type=int, default=200,
+                    help="length of the event-timed pass that feeds roofline (2-ply: min(this, 50))")
     args = ap.parse_args()
 
     world, rank, local = init_dist()
@@ -202,7 +204,7 @@ def main():
 
     el, d, tm, d_tm, gathered = run_engine(args, world, rank, args.ply, args.k_top, args.lanes, args.steps,
                                            args.warmup, args.harvest_every, timing=True,
-                                           timing_steps=min(args.steps, 200))
+                                           timing_steps=min(args.steps, args.timing_steps))
     el = max_over_ranks(el, world)
     total_steps = sum_over_ranks(d["env_steps"], world)
     value = total_steps / el
@@ -212,7 +214,7 @@ def main():
     if args.two_ply_steps > 0 and args.ply == 1:
         el2, d2, tm2, d2_tm, _ = run_engine(args, world, rank, 2, 4, args.lanes, args.two_ply_steps, 20,
                                             args.harvest_every, timing=True,
-                                            timing_steps=min(args.two_ply_steps, 50))
+                                            timing_steps=min(args.two_ply_steps, args.timing_steps, 50))
         el2 = max_over_ranks(el2, world)
         tot2 = sum_over_ranks(d2["env_steps"], world)
         r2, k2 = roofline_for(d2_tm, tm2)

@@ -423,8 +423,7 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
 // heavy_t: a doubles level with more children than this returns -2 (the
 // small-launch kernel then expands the job with the whole block)
 template <bool G>
-BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc,
-                    int heavy_t = 0x7FFFFFFF) {
+BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int heavy_t) {
     const Root& R = in.R;
     const int l = lane_id();
     const Node root = root_node(R);
@@ -543,16 +542,32 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
             }
         }
     }
-    const int base = begin_emit(a, j, nfin, fc);
-    if (base < 0) return nfin;
+    fin_out = fin;
+    return nfin;
+}
+
+// write the job's records (keys in `fin`) as boards at rows base..base+nfin-1
+template <bool G>
+BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const uint32_t* fin, int nfin, int base) {
+    const bool dbl = in.d0 == in.d1;
     for (int b = 0; b < nfin; b += 64) {
-        const int i = b + l;
+        const int i = b + lane_id();
         if (i < nfin) {
             const uint32_t e = ld32<G>(fin + i);
-            const Node n = dbl ? rebuild(R, e & KEYMASK, d) : nd_board(R, e);
-            emit_one(a, j, R, n, i, base);
+            const Node n = dbl ? rebuild(in.R, e & KEYMASK, in.d0) : nd_board(in.R, e);
+            emit_one(a, j, in.R, n, i, base);
         }
     }
+}
+
+template <bool G>
+BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc,
+                    int heavy_t = 0x7FFFFFFF) {
+    uint32_t* fin = nullptr;
+    const int nfin = job_records<G>(in, M, fin, heavy_t);
+    if (nfin < 0) return nfin;
+    const int base = begin_emit(a, j, nfin, fc);
+    if (base >= 0) emit_records<G>(a, j, in, fin, nfin, base);
     return nfin;
 }
 
@@ -758,6 +773,81 @@ __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
     }
 }
 
+// Tier 1 for launches with few jobs (the 1-ply step, the first 2-ply launch):
+// 16-wave blocks, one job per wave per window. The block reserves its rows of
+// the flat output with ONE atomic (a same-address global atomic costs ~11 ns
+// in series: one per job would serialise 4,096 jobs for ~45 us) and each
+// wave writes its records at its prefix within the block.
+__global__ __launch_bounds__(NTH) void movegen_few_kernel(MovegenArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[BW * Slice<S_T1>::bytes / 8];
+    __shared__ uint32_t wcnt[BW];
+    __shared__ int base_s;
+    const int w = (int)threadIdx.x >> 6, l = lane_id();
+    const int n_jobs = uniform(job_count(a));
+    unsigned long long* sl = smem + (size_t)w * (Slice<S_T1>::bytes / 8);
+    Mem M;
+    M.tab = sl;
+    M.F = Slice<S_T1>::F;
+    M.fa = (uint32_t*)(sl + S_T1);
+    M.fb = M.fa + M.F;
+    M.map = M.fb + M.F;
+    M.S = S_T1;
+    M.map[l] = 0u;
+    for (int win = (int)blockIdx.x; win * BW < n_jobs; win += (int)gridDim.x) {
+        const int j = win * BW + w;
+        int nf = 0;
+        bool emit = false;
+        uint32_t* fin = nullptr;
+        JobIn in;
+        if (j < n_jobs) {
+            in = fetch_job(a, j);
+            if (in.skip) {
+                emit = true;
+            } else {
+                const int r = a.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, a.heavy_t);
+                if (r < 0) {
+                    if (l == 0) push_ovf(a, j);   // overflow or heavy doubles: tier 2 owns the job
+                } else {
+                    emit = true;
+                    nf = r;
+                }
+            }
+        }
+        if (l == 0) wcnt[w] = emit ? (uint32_t)nf : 0u;
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < BW; ++k) {
+            const int c = (int)wcnt[k];
+            before += k < w ? c : 0;
+            total += c;
+        }
+        if (a.out_mode == OUT_PACKED_FLAT) {
+            if (threadIdx.x == 0) {
+                int base = total ? (int)atomicAdd(a.flat_count, (unsigned)total) : 0;
+                if (base + total > a.flat_cap) {
+                    atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
+                    base = -1;
+                }
+                base_s = base;
+            }
+            __syncthreads();
+            const int base = base_s;
+            if (emit) {
+                if (l == 0) {
+                    a.job_off[j] = base < 0 ? 0 : base + before;
+                    a.job_cnt[j] = base < 0 ? 0 : nf;
+                }
+                if (base >= 0 && nf) emit_records<false>(a, j, in, fin, nf, base + before);
+            }
+        } else if (emit) {
+            if (l == 0) a.out_count[j] = nf;
+            if (nf) emit_records<false>(a, j, in, fin, nf, 0);
+        }
+        __syncthreads();   // the slices are reused by the next window
+    }
+}
+
 // Tier 2, one 16-wave block per listed job: doubles are expanded by the
 // whole block (coop_doubles); a non-doubles job runs in wave 0 in a 32 KB
 // slice. A job that still does not fit (tier 3) runs in wave 0 over the
@@ -839,28 +929,41 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         e = hipMemsetAsync(a.ovf_count, 0, sizeof(unsigned), stream);
         if (e != hipSuccess) return e;
     }
-    // persistent grid: as many one-wave blocks as the CU admits (LDS, registers, 32 waves)
-    static int per_cu1 = 0, per_cub = 0;
+    // resident blocks per CU of each kernel (LDS, registers, 32 waves)
+    static int per_cu1 = 0, per_cub = 0, per_cuf = 0;
     if (!per_cu1) {
         auto occ = [](int& n, const void* k, int threads, int dflt) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n <= 0) n = dflt;
         };
         occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 64, 20);
         occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
+        occ(per_cuf, (const void*)bgx::movegen_few_kernel, bgx::NTH, 1);
     }
     // test hook: route every job to tier 2 (2) or tier 3 (3)
     if (const char* v = getenv("BGX_MG_TEST_TIER")) a.force_tier = atoi(v);
-    // heavy doubles go to the block-cooperative tier 2 when the launch is
-    // latency-bound (BGX_MG_COOP=1/0 forces it on/off)
     int coop = -1;
     if (const char* v = getenv("BGX_MG_COOP")) coop = atoi(v);
-    int blocks = n_cu * per_cu1;
-    const bool few = !a.n_jobs_dev && a.n_jobs <= blocks;
+    // latency-bound launches (at most 4 windows of 16 jobs per CU, host-known
+    // count): tier 1 in 16-wave blocks with one flat-row atomic per block
+    // (BGX_MG_FEW=0/1 forces the per-wave / per-block kernel)
+    int fewm = -1;
+    if (const char* v = getenv("BGX_MG_FEW")) fewm = atoi(v);
+    const bool few_jobs = !a.n_jobs_dev && a.n_jobs <= n_cu * per_cuf * bgx::BW * 4;
+    const bool few = fewm == 1 || (fewm < 0 && few_jobs);
     int heavy = bgx::HEAVY_T;
     if (const char* v = getenv("BGX_MG_HEAVY_T")) heavy = atoi(v);
-    a.heavy_t = (coop == 1 || (coop < 0 && few)) ? heavy : 0x7FFFFFFF;
-    if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
-    hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
+    // heavy doubles go to the block-cooperative tier 2 when the launch is
+    // latency-bound (BGX_MG_COOP=1/0 forces it on/off)
+    a.heavy_t = (coop == 1 || (coop < 0 && few_jobs)) ? heavy : 0x7FFFFFFF;
+    if (few) {
+        int blocks = a.n_jobs_dev ? n_cu * per_cuf : (a.n_jobs + bgx::BW - 1) / bgx::BW;
+        if (blocks > n_cu * per_cuf) blocks = n_cu * per_cuf;
+        hipLaunchKernelGGL(bgx::movegen_few_kernel, dim3(blocks), dim3(bgx::NTH), 0, stream, a);
+    } else {
+        int blocks = n_cu * per_cu1;
+        if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
+        hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     // tier 2 (+ tier 3 in the same block): one block per CU, at most one per workspace slice

@@ -32,10 +32,14 @@ def _run_movegen(ops, boards, player, dice, cap):
     return out.cpu().numpy(), cnt.cpu().numpy()
 
 
-@pytest.mark.parametrize("coop", ["0", "1"])
-def test_movegen_golden_cases(bgx_ops, coop, monkeypatch):
-    """Heavy doubles jobs expanded per wave (0) or handed to the
-    block-cooperative tier (1)."""
+# tier-1 kernel (per-wave "0" / 16-wave block "1") x heavy-doubles hand-off to
+# the block-cooperative tier 2 (off "0" / on "1")
+MG_MODES = [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")]
+
+
+@pytest.mark.parametrize("few,coop", MG_MODES)
+def test_movegen_golden_cases(bgx_ops, few, coop, monkeypatch):
+    monkeypatch.setenv("BGX_MG_FEW", few)
     monkeypatch.setenv("BGX_MG_COOP", coop)
     d = golden("movegen_cases.npz")
     out, cnt = _run_movegen(bgx_ops, d["boards"], d["player"], d["dice"], cap=1024)
@@ -87,8 +91,9 @@ def _fuzz_positions(seed, n_games):
     return pos
 
 
-@pytest.mark.parametrize("coop", ["0", "1"])
-def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, coop, monkeypatch):
+@pytest.mark.parametrize("few,coop", [("0", "0"), ("1", "1")])
+def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, few, coop, monkeypatch):
+    monkeypatch.setenv("BGX_MG_FEW", few)
     monkeypatch.setenv("BGX_MG_COOP", coop)
     pos = _fuzz_positions(1234, 40)
     rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
