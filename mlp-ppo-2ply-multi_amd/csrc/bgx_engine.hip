@@ -334,24 +334,28 @@ __global__ __launch_bounds__(256) void select_kernel(EngineDev e) {
     if (l == 0) e.action[i] = k4 ? e.sel[4 * i + pick] - base : pick;
 }
 
-// 2-ply: top-4 candidates by 1-ply V (torch.topk, sorted; ties -> lower index)
+// 2-ply: top-4 candidates by 1-ply V (torch.topk, sorted; ties -> lower
+// index). One wave per lane: each lane keeps the top 4 of its strided
+// candidates, then four wave-argmax rounds (value, then lower index) pop the
+// overall best.
 __global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.x * 4 + ((int)threadIdx.x >> 6);
     if (i >= e.L) return;
+    const int l = lane_id();
     const int n_full = e.cand_cnt[i];
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
     const int base = e.L + e.cand_off[i];
     if (n < 4) {
-        for (int c = 0; c < 4; ++c) e.sel[4 * i + c] = -1;
+        if (l < 4) e.sel[4 * i + l] = -1;
         return;
     }
     float bv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    int bi[4] = {-1, -1, -1, -1};
-    for (int k = 0; k < n; ++k) {
+    int bi[4] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+    for (int k = l; k < n; k += 64) {   // ascending k per lane: strict > keeps the lower index first
         const float v = e.V[base + k];
-        if (bi[3] >= 0 && !(v > bv[3])) continue;
+        if (bi[3] != 0x7FFFFFFF && !(v > bv[3])) continue;
         int pos = 3;
-        while (pos > 0 && (bi[pos - 1] < 0 || v > bv[pos - 1])) {
+        while (pos > 0 && (bi[pos - 1] == 0x7FFFFFFF || v > bv[pos - 1])) {
             bv[pos] = bv[pos - 1];
             bi[pos] = bi[pos - 1];
             --pos;
@@ -359,11 +363,30 @@ __global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
         bv[pos] = v;
         bi[pos] = k;
     }
-    for (int c = 0; c < 4; ++c) e.sel[4 * i + c] = base + bi[c];
+    int out = 0;
+    for (int c = 0; c < 4; ++c) {
+        float v = bv[0];
+        int k = bi[0];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float ov = __shfl_xor(v, off, 64);
+            const int ok = __shfl_xor(k, off, 64);
+            if (ov > v || (ov == v && ok < k)) { v = ov; k = ok; }
+        }
+        if (l == c) out = k;
+        if (bi[0] == k) {   // the owning lane pops its head
+            bv[0] = bv[1]; bv[1] = bv[2]; bv[2] = bv[3]; bv[3] = -INFINITY;
+            bi[0] = bi[1]; bi[1] = bi[2]; bi[2] = bi[3]; bi[3] = 0x7FFFFFFF;
+        }
+    }
+    if (l < 4) e.sel[4 * i + l] = base + out;
 }
 
 // 2-ply: per (candidate, roll) job, mean of the top-5 reply values
-// (two_ply.py:133-142); 0 when the opponent has no move (the roll adds nothing)
+// (two_ply.py:133-142); 0 when the opponent has no move (the roll adds nothing).
+// 16 lanes per job (coalesced loads); each lane keeps its top 5, then five
+// group-max rounds pop the job's top 5 in descending order (the reference's
+// summation order).
 __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    const int32_t* __restrict__ job_off,
                                                    const int32_t* __restrict__ job_cnt, int n_jobs,
@@ -372,25 +395,40 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
     int nj = n_jobs;
     if (n_units_dev) nj += (int)(*n_units_dev) * jobs_per_unit;
     if (nj > max_jobs) nj = max_jobs;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nj; j += gridDim.x * blockDim.x) {
-        const int c = job_cnt[j], o = job_off[j];
-        float t0 = -INFINITY, t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY, t4 = -INFINITY;
-        for (int k = 0; k < c; ++k) {
+    const int gl = lane_id() & 15, q = lane_id() >> 4;
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int n_waves = (int)((gridDim.x * blockDim.x) >> 6);
+    // a wave takes 4 consecutive jobs per iteration; all its lanes stay in the
+    // loop (group shuffles), lanes of jobs past nj are inert
+    for (int jb = 4 * wave; jb < nj; jb += 4 * n_waves) {
+        const int j = jb + q;
+        const bool live = j < nj;
+        const int c = live ? job_cnt[j] : 0, o = live ? job_off[j] : 0;
+        float t[5] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        for (int k = gl; k < c; k += 16) {
             const float v = V[o + k];
-            if (!(v > t4)) continue;
-            if (v > t0) { t4 = t3; t3 = t2; t2 = t1; t1 = t0; t0 = v; }
-            else if (v > t1) { t4 = t3; t3 = t2; t2 = t1; t1 = v; }
-            else if (v > t2) { t4 = t3; t3 = t2; t2 = v; }
-            else if (v > t3) { t4 = t3; t3 = v; }
-            else { t4 = v; }
+            if (!(v > t[4])) continue;
+            if (v > t[0]) { t[4] = t[3]; t[3] = t[2]; t[2] = t[1]; t[1] = t[0]; t[0] = v; }
+            else if (v > t[1]) { t[4] = t[3]; t[3] = t[2]; t[2] = t[1]; t[1] = v; }
+            else if (v > t[2]) { t[4] = t[3]; t[3] = t[2]; t[2] = v; }
+            else if (v > t[3]) { t[4] = t[3]; t[3] = v; }
+            else { t[4] = v; }
         }
         const int m = c < 5 ? c : 5;
-        float s = t0;
-        if (m > 1) s += t1;
-        if (m > 2) s += t2;
-        if (m > 3) s += t3;
-        if (m > 4) s += t4;
-        out[j] = m ? s / (float)m : 0.0f;
+        float s = 0.0f;
+        for (int r = 0; r < 5; ++r) {
+            float v = t[0];
+            int who = gl;
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1) {
+                const float ov = __shfl_xor(v, off, 64);
+                const int ow = __shfl_xor(who, off, 64);
+                if (ov > v || (ov == v && ow < who)) { v = ov; who = ow; }
+            }
+            if (r < m) s = r ? s + v : v;
+            if (who == gl) { t[0] = t[1]; t[1] = t[2]; t[2] = t[3]; t[3] = t[4]; t[4] = -INFINITY; }
+        }
+        if (live && gl == 0) out[j] = m ? s / (float)m : 0.0f;
     }
 }
 
@@ -437,15 +475,15 @@ extern "C" hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t str
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::topk_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);
+    hipLaunchKernelGGL(bgx::topk_kernel, dim3((e->L + 3) / 4), dim3(256), 0, stream, *e);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt,
                                       int n_jobs, const unsigned* n_units_dev, int jobs_per_unit,
                                       int max_jobs, float* out, hipStream_t stream) {
     if (max_jobs <= 0) return hipSuccess;
-    int blocks = (max_jobs + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
+    int blocks = (max_jobs + 15) / 16;   // 16 jobs per 256-thread block
+    if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
                        n_units_dev, jobs_per_unit, max_jobs, out);
     return hipGetLastError();
