@@ -83,16 +83,30 @@ BGX_DEV uint4 lut_entry(uint32_t b) {
     return *(const uint4*)&f;
 }
 
-// NT = boards tiles of 32 per wave iteration (1: latency-bound small batches,
-// 2: throughput; each A fragment read from LDS then feeds 2 MFMAs).
-template <int NT>
-__global__ __launch_bounds__(512) void mlp_kernel(MlpArgs a) {
+BGX_DEV void load_rows(const MlpArgs& a, int n, int t, int NTq, int col, uint4& x, uint4& y) {
+    const int row = t * 32 + col;
+    x = make_uint4(0, 0, 0, 0);
+    y = make_uint4(0, 0, 0, 0);
+    (void)NTq;
+    if (row < n) {
+        const uint4* p = (const uint4*)(a.rows + (size_t)row * 8);
+        x = p[0];
+        y = p[1];
+    }
+}
+
+// NT = board tiles of 32 per wave iteration (1: latency-bound small batches,
+// 2: throughput; each A fragment read from LDS then feeds 2 MFMAs); NW =
+// waves per block (one persistent block per CU). The next tile's rows and the
+// next k-step's A / feature fragments are loaded while the current k-step's
+// MFMAs run.
+template <int NT, int NW>
+__global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
     uint4* wf = lds;                                   // [NFRAG]
     uint4* lut = lds + NFRAG;                          // [256]
     for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i);
-    __syncthreads();
 
     int n = a.n_rows;
     if (a.n_rows_dev) n += (int)*a.n_rows_dev;
@@ -102,19 +116,19 @@ __global__ __launch_bounds__(512) void mlp_kernel(MlpArgs a) {
     const int h = lane >> 5;
     const int col = lane & 31;
     const int wave = threadIdx.x >> 6;
-    const int waves = blockDim.x >> 6;
-    for (int t = blockIdx.x * waves + wave; t < tiles; t += gridDim.x * waves) {
+    const int nwaves = gridDim.x * NW;
+    int t = blockIdx.x * NW + wave;
+    uint4 px[NT], py[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) load_rows(a, n, t * NT + q, NT, col, px[q], py[q]);
+    __syncthreads();
+    for (; t < tiles; t += nwaves) {
         uint4 bx[NT], by[NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
-            const int row = (t * NT + q) * 32 + col;
-            bx[q] = make_uint4(0, 0, 0, 0);
-            by[q] = make_uint4(0, 0, 0, 0);
-            if (row < n) {
-                const uint4* p = (const uint4*)(a.rows + (size_t)row * 8);
-                bx[q] = p[0];
-                by[q] = p[1];
-            }
+            bx[q] = px[q];
+            by[q] = py[q];
+            load_rows(a, n, (t + nwaves) * NT + q, NT, col, px[q], py[q]);   // next tile
         }
         floatx16 acc[4][NT];
 #pragma unroll
@@ -123,25 +137,34 @@ __global__ __launch_bounds__(512) void mlp_kernel(MlpArgs a) {
             for (int q = 0; q < NT; ++q)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[m][q][r] = 0.0f;
+        // fragment pipeline at (k-step, m-tile) granularity: the next (hi, lo)
+        // A pair is read from LDS while the current pair's MFMAs run
+        uint4 ch = wf[((0 * 4 + 0) * KSTEPS + 0) * 64 + lane];
+        uint4 cl = wf[((1 * 4 + 0) * KSTEPS + 0) * 64 + lane];
+        half8 b[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) b[q] = feat_frag(bx[q], by[q], 0, h, lut);
 #pragma unroll 1
         for (int s = 0; s < KSTEPS; ++s) {
-            uint4 ah[4], al[4];
+            const int sn = s + 1 < KSTEPS ? s + 1 : s;
+            half8 nb[NT];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) nb[q] = feat_frag(bx[q], by[q], sn, h, lut);
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                ah[m] = wf[((0 * 4 + m) * KSTEPS + s) * 64 + lane];
-                al[m] = wf[((1 * 4 + m) * KSTEPS + s) * 64 + lane];
-            }
-            half8 b[NT];
-#pragma unroll
-            for (int q = 0; q < NT; ++q) b[q] = feat_frag(bx[q], by[q], s, h, lut);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
+                const int s2 = m < 3 ? s : sn, m2 = m < 3 ? m + 1 : 0;
+                const uint4 nh = wf[((0 * 4 + m2) * KSTEPS + s2) * 64 + lane];
+                const uint4 nl = wf[((1 * 4 + m2) * KSTEPS + s2) * 64 + lane];
 #pragma unroll
                 for (int q = 0; q < NT; ++q) {
-                    acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah[m], b[q], acc[m][q], 0, 0, 0);
-                    acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al[m], b[q], acc[m][q], 0, 0, 0);
+                    acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ch, b[q], acc[m][q], 0, 0, 0);
+                    acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&cl, b[q], acc[m][q], 0, 0, 0);
                 }
+                ch = nh;
+                cl = nl;
             }
+#pragma unroll
+            for (int q = 0; q < NT; ++q) b[q] = nb[q];
         }
         float v[NT];
 #pragma unroll
@@ -219,10 +242,10 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
-        if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-                hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-                hipSuccess)
+        if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)bgx::mlp_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds) != hipSuccess)
             return hipErrorInvalidValue;
     }
     static int nt_override = -1;
@@ -231,17 +254,18 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
         nt_override = v ? atoi(v) : 0;
     }
     const int nt = (nt_override ? nt_override : args->nt) == 2 ? 2 : 1;
+    const int nw = nt == 2 ? 8 : 16;
     int blocks = n_cu;
     if (!args->n_rows_dev) {
         const int tiles = (args->n_rows + 32 * nt - 1) / (32 * nt);
-        const int need = (tiles + 7) / 8;
+        const int need = (tiles + nw - 1) / nw;
         if (need < blocks) blocks = need;
         if (blocks <= 0) return hipSuccess;
     }
     if (nt == 2)
-        hipLaunchKernelGGL(bgx::mlp_kernel<2>, dim3(blocks), dim3(512), lds, stream, *args);
+        hipLaunchKernelGGL((bgx::mlp_kernel<2, 8>), dim3(blocks), dim3(512), lds, stream, *args);
     else
-        hipLaunchKernelGGL(bgx::mlp_kernel<1>, dim3(blocks), dim3(512), lds, stream, *args);
+        hipLaunchKernelGGL((bgx::mlp_kernel<1, 16>), dim3(blocks), dim3(1024), lds, stream, *args);
     return hipGetLastError();
 }
 
