@@ -56,12 +56,14 @@ struct bgx_net {
     float b2 = 0.0f;
     uint4* wfrag = nullptr;   // split-fp16 MFMA fragments
     float* rowc = nullptr;    // [128] w2
-    float acc_to_exp2 = 0.0f; // -2^-e log2(e)
+    float feat_scale = 1.0f;  // 2^-e: features scaled so the accumulator is the exp2 argument
     uint32_t* scratch = nullptr;   // packed boards for bgx_value_boards
     int scratch_n = 0;
 };
 
 // Split-fp16 fragments (see bgx_mlp.hip header for the scheme). Returns e.
+static constexpr double kLog2e = 1.4426950408889634;
+
 static int build_fragments(const float* W1, const float* b1, std::vector<uint16_t>& frag) {
     std::vector<double> Wp(128 * 208, 0.0);
     double mx = 0.0;
@@ -69,16 +71,19 @@ static int build_fragments(const float* W1, const float* b1, std::vector<uint16_
         for (int k = 0; k < 198; ++k) {
             double v = W1[j * 198 + k];
             if (k == 193 || k == 195) v /= 15.0;   // feature = integer borne-off count
-            Wp[j * 208 + k] = v;
+            Wp[j * 208 + k] = -kLog2e * v;          // accumulator = -h log2(e): sigmoid = 1 / (1 + 2^acc)
         }
-        Wp[j * 208 + 198] = b1[j];                 // bias column, constant 1.0 feature
+        Wp[j * 208 + 198] = -kLog2e * b1[j];       // bias column, constant feature
         for (int k = 0; k < 208; ++k) mx = std::fmax(mx, std::fabs(Wp[j * 208 + k]));
     }
+    // W scaled by 2^e (largest |w| in [2^14, 2^15)), features by 2^-e; e <= 13
+    // keeps the smallest feature (0.5 * 2^-e) a normal fp16, e >= -11 keeps the
+    // largest (15 * 2^-e) finite
     int e = 0;
     if (mx > 0.0) {
         e = 14 - (int)std::floor(std::log2(mx));
-        if (e > 100) e = 100;
-        if (e < -100) e = -100;
+        if (e > 13) e = 13;
+        if (e < -11) e = -11;
     }
     const double sc = std::ldexp(1.0, e);
     std::vector<_Float16> hi(128 * 208), lo(128 * 208);
@@ -107,7 +112,7 @@ static int build_fragments(const float* W1, const float* b1, std::vector<uint16_
 static int net_upload(bgx_net* n, const float* W1, const float* b1, const float* w2, const float* b2) {
     std::vector<uint16_t> frag;
     const int e = build_fragments(W1, b1, frag);
-    n->acc_to_exp2 = (float)(-std::ldexp(1.0, -e) * 1.4426950408889634);
+    n->feat_scale = (float)std::ldexp(1.0, -e);
     HIP_TRY(hipMemcpy(n->W1, W1, 128 * 198 * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(n->b1, b1, 128 * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(n->w2, w2, 128 * 4, hipMemcpyHostToDevice));
@@ -287,7 +292,7 @@ int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t
     m.wfrag = net->wfrag;
     m.rowc = net->rowc;
     m.b2 = net->b2;
-    m.acc_to_exp2 = net->acc_to_exp2;
+    m.feat_scale = net->feat_scale;
     HIP_TRY(bgx_launch_mlp(&m, (hipStream_t)stream));
     return BGX_OK;
 }
@@ -358,7 +363,7 @@ int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_op
         m.wfrag = net->wfrag;
         m.rowc = net->rowc;
         m.b2 = net->b2;
-        m.acc_to_exp2 = net->acc_to_exp2;
+        m.feat_scale = net->feat_scale;
         if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
     }
     if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, s) != hipSuccess) rc = BGX_E_HIP;
@@ -584,7 +589,7 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
         m.wfrag = e->net->wfrag;
         m.rowc = e->net->rowc;
         m.b2 = e->net->b2;
-        m.acc_to_exp2 = e->net->acc_to_exp2;
+        m.feat_scale = e->net->feat_scale;
         if (timed(e, 1, s, true)) return BGX_E_HIP;
         HIP_TRY(bgx_launch_mlp(&m, s));
         if (timed(e, 1, s, false)) return BGX_E_HIP;
@@ -627,7 +632,7 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             r.wfrag = e->net->wfrag;
             r.rowc = e->net->rowc;
             r.b2 = e->net->b2;
-            r.acc_to_exp2 = e->net->acc_to_exp2;
+            r.feat_scale = e->net->feat_scale;
             if (timed(e, 1, s, true)) return BGX_E_HIP;
             HIP_TRY(bgx_launch_mlp(&r, s));
             if (timed(e, 1, s, false)) return BGX_E_HIP;

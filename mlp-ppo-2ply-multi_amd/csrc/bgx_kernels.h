@@ -62,7 +62,7 @@ struct MlpArgs {
     const uint4* wfrag;          // [2][4][13][64] fragments (16 B each)
     const float* rowc;           // [128] w2 (value_head.weight)
     float b2;
-    float acc_to_exp2;           // -2^-e * log2(e): accumulator -> exp2 argument of exp(-h)
+    float feat_scale;            // 2^-e: features are scaled so the accumulator is -h log2(e)
 };
 
 // Self-play lane state (one engine per device), structure of arrays.

@@ -7,11 +7,13 @@
 // Numerics ("split fp16"). Every live feature is exact in fp16
 // once the two borne-off columns (193, 195) take the integer count k and W1's
 // columns are pre-divided by 15; b1 rides in the K padding as column 198 with
-// a constant 1.0 feature. W1 is scaled by one power of two 2^e (largest |w| in
-// [2^14, 2^15): no fp16 overflow; residues below the fp16 normal range carry
-// absolute errors ~2^-25 / 2^e, negligible) and split W = W_hi + W_lo, both
-// fp16; the MFMA multiplies are exact and accumulate in fp32, so two passes
-// give ~fp32 accuracy (|dV| < 1e-5 on the trained checkpoint).
+// a constant feature. W1 is pre-multiplied by -log2(e) (so the accumulator is
+// directly the exp2 argument of the sigmoid) and by one power of two 2^e
+// (largest |w| in [2^14, 2^15), e capped at 13), the features by 2^-e (still
+// exact: multiples of 0.5 * 2^-e, normal for e <= 13); residues below the fp16
+// normal range carry absolute errors ~2^-25 / 2^e, negligible. W = W_hi + W_lo,
+// both fp16; the MFMA multiplies are exact and accumulate in fp32, so two
+// passes give ~fp32 accuracy (|dV| < 1e-5 on the trained checkpoint).
 //
 // Features for k-steps 0..11 come from a 256-entry LDS table: one byte of the
 // packed board = the counts of two adjacent point slots -> their 8 fp16
@@ -40,7 +42,7 @@ constexpr int NFRAG = 2 * 4 * KSTEPS * 64;
 BGX_DEV _Float16 hf(float v) { return (_Float16)v; }
 
 // B fragment (8 features of one board) for k-step s (0..12), lane half h
-BGX_DEV half8 feat_frag(const uint4 x, const uint4 y, int s, int h, const uint4* lut) {
+BGX_DEV half8 feat_frag(const uint4 x, const uint4 y, int s, int h, const uint4* lut, float sc) {
     if (s < 12) {
         // point slots q0 = 4s + 2h and q0 + 1 = byte (2(s&1) + h) of word s >> 1
         const int wi = s >> 1;
@@ -56,7 +58,7 @@ BGX_DEV half8 feat_frag(const uint4 x, const uint4 y, int s, int h, const uint4*
     }
     half8 f;
     const uint32_t s6 = y.z;
-    const float on = h == 0 ? 1.0f : 0.0f;
+    const float on = h == 0 ? sc : 0.0f;   // features carry the 2^-e scale
     const uint32_t flag = (s6 >> 16) & 1u;
     f[0] = hf(on * (float)(s6 & 15u) * 0.5f);          // bar1 / 2
     f[1] = hf(on * (float)((s6 >> 8) & 15u));          // off1 (W col / 15)
@@ -69,16 +71,17 @@ BGX_DEV half8 feat_frag(const uint4 x, const uint4 y, int s, int h, const uint4*
     return f;
 }
 
-// LUT entry for byte b: features [n>=1, n>=2, n>=3, max(n-3,0)/2] of n = b & 15, then of b >> 4
-BGX_DEV uint4 lut_entry(uint32_t b) {
+// LUT entry for byte b: features [n>=1, n>=2, n>=3, max(n-3,0)/2] of n = b & 15, then of b >> 4,
+// times the 2^-e scale
+BGX_DEV uint4 lut_entry(uint32_t b, float sc) {
     half8 f;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int n = (int)((b >> (4 * t)) & 15u);
-        f[4 * t + 0] = n >= 1 ? (_Float16)1.0f : (_Float16)0.0f;
-        f[4 * t + 1] = n >= 2 ? (_Float16)1.0f : (_Float16)0.0f;
-        f[4 * t + 2] = n >= 3 ? (_Float16)1.0f : (_Float16)0.0f;
-        f[4 * t + 3] = (_Float16)(n > 3 ? (float)(n - 3) * 0.5f : 0.0f);
+        f[4 * t + 0] = (_Float16)(n >= 1 ? sc : 0.0f);
+        f[4 * t + 1] = (_Float16)(n >= 2 ? sc : 0.0f);
+        f[4 * t + 2] = (_Float16)(n >= 3 ? sc : 0.0f);
+        f[4 * t + 3] = (_Float16)(n > 3 ? (float)(n - 3) * 0.5f * sc : 0.0f);
     }
     return *(const uint4*)&f;
 }
@@ -106,7 +109,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
     uint4* wf = lds;                                   // [NFRAG]
     uint4* lut = lds + NFRAG;                          // [256]
     for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i);
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i, a.feat_scale);
 
     int n = a.n_rows;
     if (a.n_rows_dev) n += (int)*a.n_rows_dev;
@@ -143,13 +146,13 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
         uint4 cl = wf[((1 * 4 + 0) * KSTEPS + 0) * 64 + lane];
         half8 b[NT];
 #pragma unroll
-        for (int q = 0; q < NT; ++q) b[q] = feat_frag(bx[q], by[q], 0, h, lut);
+        for (int q = 0; q < NT; ++q) b[q] = feat_frag(bx[q], by[q], 0, h, lut, a.feat_scale);
 #pragma unroll 1
         for (int s = 0; s < KSTEPS; ++s) {
             const int sn = s + 1 < KSTEPS ? s + 1 : s;
             half8 nb[NT];
 #pragma unroll
-            for (int q = 0; q < NT; ++q) nb[q] = feat_frag(bx[q], by[q], sn, h, lut);
+            for (int q = 0; q < NT; ++q) nb[q] = feat_frag(bx[q], by[q], sn, h, lut, a.feat_scale);
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const int s2 = m < 3 ? s : sn, m2 = m < 3 ? m + 1 : 0;
@@ -169,10 +172,9 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
         float v[NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) v[q] = 0.0f;
-        // sigmoid(h) = 1 / (1 + 2^(acc * -2^-e log2 e)); w2 per hidden row by wave-uniform
-        // (scalar) loads of rows j0 and j0 + 4, picked by lane half
+        // sigmoid(h) = 1 / (1 + 2^acc) (acc = -h log2 e); w2 per hidden row by
+        // wave-uniform (scalar) loads of rows j0 and j0 + 4, picked by lane half
         const float* w2 = a.rowc;
-        const float ks = a.acc_to_exp2;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
 #pragma unroll
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
                 const float cy = h ? w2[j0 + 4] : w2[j0];
 #pragma unroll
                 for (int q = 0; q < NT; ++q) {
-                    const float ex = __builtin_amdgcn_exp2f(acc[m][q][r] * ks);
+                    const float ex = __builtin_amdgcn_exp2f(acc[m][q][r]);
                     v[q] = fmaf(cy, __builtin_amdgcn_rcpf(1.0f + ex), v[q]);
                 }
                 if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);

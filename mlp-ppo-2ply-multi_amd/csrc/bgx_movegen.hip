@@ -631,34 +631,39 @@ BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin) {
     __syncthreads();
     int n = 1, level = 0;
     while (level < 4) {
-        // 1. parents 2t, 2t + 1
-        int c[2];
-        uint32_t src[2], pack[2];
+        // 1. parents t and t + NTH (waves past the level skip the work)
+        const int w = t >> 6;
+        int c[2] = {0, 0};
+        uint32_t src[2] = {0u, 0u}, pack[2] = {0u, 0u};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = 2 * t + h;
-            const uint32_t pkey = i < n ? fa[i] & KEYMASK : KEY_EMPTY4;
-            const Moves pm = node_moves(R, rebuild(R, pkey, d), d, okd);
-            c[h] = i < n ? pm.n : 0;
-            src[h] = pm.src;
-            pack[h] = (uint32_t)pm.nsrc | ((uint32_t)(pm.e0 + 1) << 5) | ((uint32_t)(pm.e1 + 1) << 10) |
-                      (pm.n == 1 ? 1u << 15 : 0u);
+        for (int hh = 0; hh < 2; ++hh) {
+            if (hh * NTH + 64 * w < n) {        // wave-uniform
+                const int i = hh * NTH + t;
+                const uint32_t pkey = i < n ? fa[i] & KEYMASK : KEY_EMPTY4;
+                const Moves pm = node_moves(R, rebuild(R, pkey, d), d, okd);
+                c[hh] = i < n ? pm.n : 0;
+                src[hh] = pm.src;
+                pack[hh] = (uint32_t)pm.nsrc | ((uint32_t)(pm.e0 + 1) << 5) | ((uint32_t)(pm.e1 + 1) << 10) |
+                           (pm.n == 1 ? 1u << 15 : 0u);
+            }
         }
-        int T;
-        const int ex0 = block_excl_scan(C, c[0] + c[1], T);
+        // one block scan of both halves (16-bit fields: T <= K_TMAX < 2^15)
+        int tot2;
+        const int ex2 = block_excl_scan(C, c[0] | (c[1] << 16), tot2);
+        const int T0 = tot2 & 0xFFFF, T = T0 + (tot2 >> 16);
         if (T == 0) break;                      // uniform
         if (T > K_TMAX) return -1;
         int S = 64;
         while (S < 2 * T && S < K_S) S <<= 1;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = 2 * t + h;
+        for (int hh = 0; hh < 2; ++hh) {
+            const int i = hh * NTH + t;
             if (i < n) {
-                const int ex = ex0 + (h ? c[0] : 0);
-                C.psrc[i] = src[h];
-                C.ppack[i] = pack[h];
+                const int ex = hh ? T0 + (ex2 >> 16) : (ex2 & 0xFFFF);
+                C.psrc[i] = src[hh];
+                C.ppack[i] = pack[hh];
                 C.pexcl[i] = (uint32_t)ex;
-                for (int k = 0; k < c[h]; ++k) C.map[ex + k] = (uint16_t)i;
+                for (int k = 0; k < c[hh]; ++k) C.map[ex + k] = (uint16_t)i;
             }
         }
         for (int i = t; i < S; i += NTH) C.tab[i] = EMPTY64;
@@ -672,6 +677,7 @@ BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin) {
         M.S = S;
         int fresh_n = 0;
         for (int b = 0; b < T; b += NTH) {     // uniform trip count
+            if (b + 64 * w >= T) break;        // wave-uniform: no children left for this wave
             const int r = b + t;
             const bool act = r < T;
             const int p = act ? (int)C.map[r] : 0;

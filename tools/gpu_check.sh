@@ -4,6 +4,7 @@ export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
 tail -2 gpurun_out/t.log
 timeout -k 10 200 python tools/mg_micro.py 200000 > gpurun_out/mg.log 2>&1 && cat gpurun_out/mg.log
+timeout -k 10 200 python tools/mg_latency.py 2>&1 | grep -v amdgpu.ids
 for sm in default; do
   timeout -k 10 300 python bench.py --steps 300 --warmup 100 --no-cpu-baseline > gpurun_out/b$sm.log 2>&1 || exit 1
   python - $sm <<'PY'
