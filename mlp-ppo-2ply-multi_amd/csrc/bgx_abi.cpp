@@ -402,7 +402,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
                   e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
                   e->d_offs, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
-                  e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->d.action};
+                  e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
     for (void* p : ps) hipFree(p);
     for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
     if (e->gexec) hipGraphExecDestroy(e->gexec);
@@ -439,7 +439,6 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     ALLOC(e->ctr, 16);
     ALLOC(e->stats, 8);
     ALLOC(d.player, L);
-    ALLOC(d.action, L);
     ALLOC(d.dice, 2 * L);
     ALLOC(d.step, L);
     ALLOC(d.flags, L);
@@ -644,8 +643,7 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
                                         e->job_val, s));
             }
         }
-        HIP_TRY(bgx_launch_select(&e->d, s));
-        HIP_TRY(bgx_launch_engine_step(&e->d, s));
+        HIP_TRY(bgx_launch_select(&e->d, s));   // select + env step (one launch)
     }
     return BGX_OK;
 }
@@ -751,9 +749,19 @@ int bgx_get_stats(bgx_engine* e, bgx_stats* out) {
     if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
     unsigned long long st[8];
     HIP_TRY(hipMemcpy(st, e->stats, sizeof(st), hipMemcpyDeviceToHost));
+    // decisions = records written, episodes = games finished: the lanes' own counters
+    const int L = e->cfg.lanes;
+    std::vector<uint32_t> rec(L), epi(L);
+    HIP_TRY(hipMemcpy(rec.data(), e->d.rec_count, (size_t)L * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(epi.data(), e->d.epi, (size_t)L * 4, hipMemcpyDeviceToHost));
+    unsigned long long dec = 0, eps = 0;
+    for (int i = 0; i < L; ++i) {
+        dec += rec[i];
+        eps += epi[i];
+    }
     out->env_steps = st[0];
-    out->decisions = st[1];
-    out->episodes = st[2];
+    out->decisions = dec;
+    out->episodes = eps;
     out->value_rows = st[3];
     out->movegen_jobs = st[4];
     out->fallback_jobs = st[5];

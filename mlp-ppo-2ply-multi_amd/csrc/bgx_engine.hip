@@ -148,115 +148,89 @@ __global__ __launch_bounds__(256) void engine_reset_kernel(EngineDev e) {
     e.harv[i] = 0;
 }
 
-__global__ __launch_bounds__(256) void engine_step_kernel(EngineDev e) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = i < e.L;
-    int decided = 0, finished = 0;
-    if (live) {
-        LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), e.rng[i]};
-        int p = e.player[i];
-        int steps = e.step[i];
-        uint32_t flags = e.flags[i];
-        uint32_t w[8];
-        load_packed(e.rows + (size_t)i * 8, w);
-        const int n_full = e.cand_cnt[i];
-        const int n = n_full < e.max_legal ? n_full : e.max_legal;
-        const int base = e.L + e.cand_off[i];
-        int d0 = e.dice[2 * i], d1 = e.dice[2 * i + 1];
-        bool done = false;
-        int win_type = 0, winner = -1;
-        if (n == 0 || e.action[i] < 0) {
-            // pass (backgammon_env.py:139-151): no experience is recorded (worker.py:106-113)
-            p ^= 1;
-            rng.roll(d0, d1);
+// One game lane's env step after its action is chosen (BackgammonEnv.step,
+// backgammon_env.py:130-221, + the worker's Experience, worker.py:101-162):
+// apply, judge, record, and on game end append the episode header and reset.
+// action < 0 (or no legal move): pass.
+BGX_DEV void step_lane(const EngineDev& e, int i, int action) {
+    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), e.rng[i]};
+    int p = e.player[i];
+    int steps = e.step[i];
+    uint32_t flags = e.flags[i];
+    uint32_t w[8];
+    load_packed(e.rows + (size_t)i * 8, w);
+    const int n_full = e.cand_cnt[i];
+    const int n = n_full < e.max_legal ? n_full : e.max_legal;
+    const int base = e.L + e.cand_off[i];
+    int d0 = e.dice[2 * i], d1 = e.dice[2 * i + 1];
+    bool done = false;
+    int win_type = 0, winner = -1;
+    if (n == 0 || action < 0) {
+        // pass (backgammon_env.py:139-151): no experience is recorded (worker.py:106-113)
+        p ^= 1;
+        rng.roll(d0, d1);
+    } else {
+        flags |= 16u << p;
+        rng.ctr++;   // the select kernel's sampling uniform
+        const int a = action;
+        uint32_t nb[8];
+        load_packed(e.rows + (size_t)(base + a) * 8, nb);
+        const int mover = p;
+        const Outcome o = judge(nb, mover, flags);
+        done = o.done;
+        if (done) { win_type = o.win_type; winner = mover; }
+        else { p ^= 1; rng.roll(d0, d1); }
+        // experience record (worker.py:149-156; Experience, episode.py:5-46)
+        const uint32_t rec = e.rec_count[i];
+        if (rec - e.harv[i] >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
+        uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
+        uint32_t before[8];
+        for (int k = 0; k < 8; ++k) before[k] = w[k];
+        set_flag(before, mover);
+        set_flag(nb, done ? mover : p);
+        store_packed(R, before);
+        store_packed(R + 8, nb);
+        const float vs = e.V[i], va = e.V[base + a];
+        const int dd0 = e.dice[2 * i], dd1 = e.dice[2 * i + 1];
+        uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
+                                 (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
+        uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
+                                     ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
+                                     ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
+                                 e.epi[i], (uint32_t)steps, (uint32_t)(e.lane_base + i));
+        ((uint4*)(R + 16))[0] = tail0;
+        ((uint4*)(R + 16))[1] = tail1;
+        e.rec_count[i] = rec + 1;
+        for (int k = 0; k < 8; ++k) w[k] = nb[k];
+    }
+    ++steps;
+    set_flag(w, p);
+    if (done || steps >= e.max_steps) {
+        const uint32_t slot = atomicAdd(e.ep_count, 1u);
+        if ((int)slot < e.ep_cap) {
+            uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
+            const uint32_t first = e.ep_first[i], nrec = e.rec_count[i] - first;
+            ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), e.epi[i], first, nrec);
+            ((uint4*)h)[1] = make_uint4((uint32_t)steps,
+                                        (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
+                                            (flags << 16),
+                                        0u, 0u);
         } else {
-            decided = 1;
-            flags |= 16u << p;
-            rng.ctr++;   // the select kernel's sampling uniform
-            const int a = e.action[i];
-            uint32_t nb[8];
-            load_packed(e.rows + (size_t)(base + a) * 8, nb);
-            const int mover = p;
-            const Outcome o = judge(nb, mover, flags);
-            done = o.done;
-            if (done) { win_type = o.win_type; winner = mover; }
-            else { p ^= 1; rng.roll(d0, d1); }
-            // experience record (worker.py:149-156; Experience, episode.py:5-46)
-            const uint32_t rec = e.rec_count[i];
-            if (rec - e.harv[i] >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
-            uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
-            uint32_t before[8];
-            for (int k = 0; k < 8; ++k) before[k] = w[k];
-            set_flag(before, mover);
-            set_flag(nb, done ? mover : p);
-            store_packed(R, before);
-            store_packed(R + 8, nb);
-            const float vs = e.V[i], va = e.V[base + a];
-            const int dd0 = e.dice[2 * i], dd1 = e.dice[2 * i + 1];
-            uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
-                                     (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
-            uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
-                                         ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
-                                         ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
-                                     e.epi[i], (uint32_t)steps, (uint32_t)(e.lane_base + i));
-            ((uint4*)(R + 16))[0] = tail0;
-            ((uint4*)(R + 16))[1] = tail1;
-            e.rec_count[i] = rec + 1;
-            for (int k = 0; k < 8; ++k) w[k] = nb[k];
+            atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
         }
-        ++steps;
-        set_flag(w, p);
-        if (done || steps >= e.max_steps) {
-            finished = 1;
-            const uint32_t slot = atomicAdd(e.ep_count, 1u);
-            if ((int)slot < e.ep_cap) {
-                uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
-                const uint32_t first = e.ep_first[i], nrec = e.rec_count[i] - first;
-                ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), e.epi[i], first, nrec);
-                ((uint4*)h)[1] = make_uint4((uint32_t)steps,
-                                            (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
-                                                (flags << 16),
-                                            0u, 0u);
-            } else {
-                atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
-            }
-            p = new_game(rng, w, d0, d1);
-            steps = 0;
-            flags = 0;
-            e.epi[i] = e.epi[i] + 1;
-            e.ep_first[i] = e.rec_count[i];
-        }
-        store_packed(e.rows + (size_t)i * 8, w);
-        e.player[i] = (uint8_t)p;
-        e.dice[2 * i] = (uint8_t)d0;
-        e.dice[2 * i + 1] = (uint8_t)d1;
-        e.step[i] = steps;
-        e.flags[i] = flags;
-        e.rng[i] = rng.ctr;
+        p = new_game(rng, w, d0, d1);
+        steps = 0;
+        flags = 0;
+        e.epi[i] = e.epi[i] + 1;
+        e.ep_first[i] = e.rec_count[i];
     }
-    // per-wave stats: [0] env steps [1] decisions [2] episodes
-    const uint64_t bl = ballot(live), bd = ballot(decided != 0), bf = ballot(finished != 0);
-    if (lane_id() == 0) {
-        atomicAdd(e.stats + 0, (unsigned long long)__popcll(bl));
-        atomicAdd(e.stats + 1, (unsigned long long)__popcll(bd));
-        atomicAdd(e.stats + 2, (unsigned long long)__popcll(bf));
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const unsigned fc = *e.flat_count;
-        unsigned long long rows = (unsigned long long)e.L + fc, jobs = (unsigned long long)e.L;
-        if (e.ply == 2) {
-            rows += *e.reply_count;
-            jobs += e.k_top == 0 ? 21ull * fc : (unsigned long long)e.n_jobs2;
-        }
-        atomicAdd(e.stats + 3, rows);
-        atomicAdd(e.stats + 4, jobs);
-        atomicAdd(e.stats + 5, (unsigned long long)*e.ovf_count + (e.ply == 2 ? *e.ovf_count2 : 0u));
-        // last kernel of the step: zero the per-step counters for the next one
-        *e.flat_count = 0u;
-        *e.reply_count = 0u;
-        *e.ovf_count = 0u;
-        *e.ovf_count2 = 0u;
-    }
+    store_packed(e.rows + (size_t)i * 8, w);
+    e.player[i] = (uint8_t)p;
+    e.dice[2 * i] = (uint8_t)d0;
+    e.dice[2 * i + 1] = (uint8_t)d1;
+    e.step[i] = steps;
+    e.flags[i] = flags;
+    e.rng[i] = rng.ctr;
 }
 
 // Action selection, one wavefront per game lane:
@@ -265,9 +239,29 @@ __global__ __launch_bounds__(256) void engine_step_kernel(EngineDev e) {
 //     W = sum_r P(r) * top-5 mean), softmax(score/T) over the four (two_ply.py
 //     hook 153-193); fewer than four moves: 1-ply;
 //   2-ply K=all: the same score for every candidate.
-// The uniform comes from the lane's Philox stream at its current counter; the
-// step kernel advances the counter past it.
-__global__ __launch_bounds__(256) void select_kernel(EngineDev e) {
+// The uniform comes from the lane's Philox stream at its current counter;
+// step_lane advances the counter past it. Lane 0 of the wave then runs the
+// lane's env step (one launch for select + step).
+__global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // per-step stats; decisions / episodes are the lanes' own counters
+        const unsigned fc = *e.flat_count;
+        unsigned long long rows = (unsigned long long)e.L + fc, jobs = (unsigned long long)e.L;
+        if (e.ply == 2) {
+            rows += *e.reply_count;
+            jobs += e.k_top == 0 ? 21ull * fc : (unsigned long long)e.n_jobs2;
+        }
+        atomicAdd(e.stats + 0, (unsigned long long)e.L);
+        atomicAdd(e.stats + 3, rows);
+        atomicAdd(e.stats + 4, jobs);
+        atomicAdd(e.stats + 5, (unsigned long long)*e.ovf_count + (e.ply == 2 ? *e.ovf_count2 : 0u));
+        // last kernel of the step: zero the per-step counters for the next one
+        // (no other wave of this kernel reads them)
+        *e.flat_count = 0u;
+        *e.reply_count = 0u;
+        *e.ovf_count = 0u;
+        *e.ovf_count2 = 0u;
+    }
     __shared__ float xs[4][512];
     const int w = threadIdx.x >> 6;
     const int i = blockIdx.x * 4 + w;
@@ -276,7 +270,7 @@ __global__ __launch_bounds__(256) void select_kernel(EngineDev e) {
     const int n_full = e.cand_cnt[i];
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
     if (n == 0) {
-        if (l == 0) e.action[i] = -1;
+        if (l == 0) step_lane(e, i, -1);
         return;
     }
     const int base = e.L + e.cand_off[i];
@@ -331,7 +325,7 @@ __global__ __launch_bounds__(256) void select_kernel(EngineDev e) {
         }
         carry += __shfl(p, 63, 64);
     }
-    if (l == 0) e.action[i] = k4 ? e.sel[4 * i + pick] - base : pick;
+    if (l == 0) step_lane(e, i, k4 ? e.sel[4 * i + pick] - base : pick);
 }
 
 // 2-ply: top-4 candidates by 1-ply V (torch.topk, sorted; ties -> lower
@@ -466,12 +460,9 @@ extern "C" hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream
     hipLaunchKernelGGL(bgx::engine_reset_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);
     return hipGetLastError();
 }
-extern "C" hipError_t bgx_launch_engine_step(const bgx::EngineDev* e, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::engine_step_kernel, dim3((e->L + 63) / 64), dim3(64), 0, stream, *e);
-    return hipGetLastError();
-}
+
 extern "C" hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::select_kernel, dim3((e->L + 3) / 4), dim3(256), 0, stream, *e);
+    hipLaunchKernelGGL(bgx::select_step_kernel, dim3((e->L + 3) / 4), dim3(256), 0, stream, *e);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream) {

@@ -100,7 +100,6 @@ struct EngineDev {
     const int32_t* cand_cnt;     // [L] full candidate count
     const float* V;              // [L + cand rows] values
     int32_t* sel;                // [L * 4] 2-ply: candidate rows chosen by 1-ply V (or -1)
-    int32_t* action;             // [L] chosen candidate index (-1 = pass), written by select
     const float* job_val;        // [L * 4 * 21] 2-ply: top-5 mean per (candidate, roll)
     unsigned* flat_count;        // candidate rows this step (device; zeroed by the step kernel)
     unsigned* reply_count;       // 2-ply reply rows this step (device; zeroed by the step kernel)
@@ -124,9 +123,8 @@ hipError_t bgx_launch_pack(const uint8_t* boards, const uint8_t* player, int n, 
                            hipStream_t stream);
 hipError_t bgx_launch_unpack(const uint32_t* packed, int n, uint8_t* out, hipStream_t stream);
 hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream_t stream);
-hipError_t bgx_launch_engine_step(const bgx::EngineDev* e, hipStream_t stream);
 hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream);
-hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream);
+hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream);   // select + env step
 hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt, int n_jobs,
                            const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
                            hipStream_t stream);
