@@ -148,13 +148,15 @@ def cpu_baseline(seconds, threads):
     return r
 
 
-def roofline_for(d, tm):
+def roofline_for(d, tm, leg):
     """Dominant kernel's algorithmic rate over its average launch (HIP events),
     from the timed pass `d` (stats deltas) / `tm` (event totals)."""
     el = d["elapsed_s"]
     mg_ms, mlp_ms = tm["movegen_ms"], tm["mlp_ms"]
     out = {}
-    mg_bytes = MOVEGEN_BYTES_PER_JOB * d["movegen_jobs"] + MOVEGEN_BYTES_PER_ROW * d["value_rows"]
+    # boards movegen wrote = value rows minus the lanes' own rows (one per lane step)
+    mg_rows = d["value_rows"] - d["env_steps"]
+    mg_bytes = MOVEGEN_BYTES_PER_JOB * d["movegen_jobs"] + MOVEGEN_BYTES_PER_ROW * mg_rows
     mg_launch = mg_ms / max(1, tm["movegen_launches"])
     out["movegen"] = {"bound": "hbm", "achieved": mg_bytes / max(1, tm["movegen_launches"]) / (mg_launch * 1e-3) / 1e9,
                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "avg_launch_ms": mg_launch,
@@ -168,13 +170,15 @@ def roofline_for(d, tm):
         v["frac"] = v["achieved"] / v["peak"]
     dom = "movegen" if mg_ms >= mlp_ms else "mlp"
     r = {k: out[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
-    r["kernel"] = "bgx::movegen_lds_kernel" if dom == "movegen" else "bgx::mlp_kernel"
+    r["kernel"] = ({"1ply": "movegen launch = bgx::movegen_few_kernel + bgx::movegen_block_kernel",
+                    "2ply": "movegen launches = (few | lds<512>) + bgx::movegen_block_kernel"}[leg]
+                   if dom == "movegen" else "bgx::mlp_kernel")
     r["traffic"] = None
     prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
             with open(prof) as f:
-                r["traffic"] = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                r["traffic"] = json.load(f).get(leg, {}).get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
             r["traffic"] = None
     return r, out
@@ -208,7 +212,7 @@ def main():
     el = max_over_ranks(el, world)
     total_steps = sum_over_ranks(d["env_steps"], world)
     value = total_steps / el
-    roof, kernels = roofline_for(d_tm, tm)
+    roof, kernels = roofline_for(d_tm, tm, f"{args.ply}ply")
 
     extra = {}
     if args.two_ply_steps > 0 and args.ply == 1:
@@ -217,7 +221,7 @@ def main():
                                             timing_steps=min(args.two_ply_steps, args.timing_steps, 50))
         el2 = max_over_ranks(el2, world)
         tot2 = sum_over_ranks(d2["env_steps"], world)
-        r2, k2 = roofline_for(d2_tm, tm2)
+        r2, k2 = roofline_for(d2_tm, tm2, "2ply")
         extra["two_ply_k4"] = {"value": tot2 / el2, "unit": "env_steps/s", "steps": args.two_ply_steps,
                                "ms_per_step": el2 / args.two_ply_steps * 1e3,
                                "value_rows_per_s": sum_over_ranks(d2["value_rows"], world) / el2,

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools only) into
+per-launch HBM bytes per leg and kernel group, with the gfx950 correction of
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE reads 1/2 of wide coalesced
+streaming reads, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+A bench "movegen launch" is tier 1 + tier 2 (movegen_few/lds + movegen_block);
+the 2-ply leg has two movegen launches and two MLP launches per step."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(path):
+    f = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    if not f:
+        return {}
+    acc = collections.defaultdict(lambda: [0.0, set()])
+    for r in csv.DictReader(open(f[0])):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        acc[name][0] += float(r["Counter_Value"])
+        acc[name][1].add(r["Dispatch_Id"])
+    return {k: (v[0], len(v[1])) for k, v in acc.items()}
+
+
+def group(name):
+    return "mlp" if "mlp_kernel" in name else "movegen"
+
+
+def main(out):
+    res = {"source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
+                     "--kernel-include-regex 'movegen|mlp_kernel', bench.py 1-ply leg (200 steps) and 2-ply leg (60 steps)",
+           "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts 1/2 of wide "
+                         "coalesced reads; narrow movegen reads are uncalibrated, the raw value is kept beside it)"}
+    for leg in ("1", "2"):
+        f = per_kernel(os.path.join(out, f"pmc_{leg}_FETCH_SIZE"))
+        w = per_kernel(os.path.join(out, f"pmc_{leg}_WRITE_SIZE"))
+        legd = {"kernels": {}}
+        for name in sorted(set(f) | set(w)):
+            fk, nf = f.get(name, (0.0, 0))
+            wk, nw = w.get(name, (0.0, 0))
+            n = max(nf, nw, 1)
+            legd["kernels"][name] = {"dispatches": n, "fetch_size_kb_per_dispatch": fk / max(nf, 1),
+                                     "write_size_kb_per_dispatch": wk / max(nw, 1)}
+        for g in ("movegen", "mlp"):
+            names = [k for k in legd["kernels"] if group(k) == g]
+            if not names:
+                continue
+            # every movegen call ends with one movegen_block_kernel dispatch; every
+            # MLP call is one mlp_kernel dispatch
+            if g == "movegen":
+                n_launch = sum(legd["kernels"][k]["dispatches"] for k in names if "movegen_block" in k)
+            else:
+                n_launch = sum(legd["kernels"][k]["dispatches"] for k in names)
+            fk = sum(legd["kernels"][k]["fetch_size_kb_per_dispatch"] * legd["kernels"][k]["dispatches"] for k in names)
+            wk = sum(legd["kernels"][k]["write_size_kb_per_dispatch"] * legd["kernels"][k]["dispatches"] for k in names)
+            legd[g] = {"kernels": names, "launches": n_launch,
+                       "hbm_bytes_per_launch": (2 * fk + wk) * 1024 / n_launch,
+                       "hbm_bytes_per_launch_uncorrected": (fk + wk) * 1024 / n_launch}
+        res[f"{leg}ply"] = legd
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
