@@ -108,8 +108,10 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
     uint4* wf = lds;                                   // [NFRAG]
     uint4* lut = lds + NFRAG;                          // [256]
+    float* w2s = (float*)(lds + NFRAG + 256);          // [128] value-head weights
     for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i, a.feat_scale);
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) w2s[i] = a.rowc[i];
 
     int n = a.n_rows;
     if (a.n_rows_dev) n += (int)*a.n_rows_dev;
@@ -172,23 +174,124 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
         float v[NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) v[q] = 0.0f;
-        // sigmoid(h) = 1 / (1 + 2^acc) (acc = -h log2 e); w2 per hidden row by
-        // wave-uniform (scalar) loads of rows j0 and j0 + 4, picked by lane half
-        const float* w2 = a.rowc;
+        // sigmoid(h) = 1 / (1 + 2^acc) (acc = -h log2 e); w2 of the lane's hidden
+        // rows j0 = 32m + (r & 3) + 8(r >> 2) + 4h from LDS, four at a time
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int j0 = 32 * m + (r & 3) + 8 * (r >> 2);
-                const float cy = h ? w2[j0 + 4] : w2[j0];
+            for (int g = 0; g < 4; ++g) {
+                const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
+                const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
-                for (int q = 0; q < NT; ++q) {
-                    const float ex = __builtin_amdgcn_exp2f(acc[m][q][r]);
-                    v[q] = fmaf(cy, __builtin_amdgcn_rcpf(1.0f + ex), v[q]);
+                for (int k = 0; k < 4; ++k) {
+                    const int r = 4 * g + k;
+#pragma unroll
+                    for (int q = 0; q < NT; ++q) {
+                        const float ex = __builtin_amdgcn_exp2f(acc[m][q][r]);
+                        v[q] = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), v[q]);
+                    }
+                    if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
                 }
-                if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
             }
         }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            v[q] += __shfl_xor(v[q], 32, 64);
+            const int row = (t * NT + q) * 32 + col;
+            if (h == 0 && row < n) a.out[row] = v[q] + a.b2;
+        }
+    }
+}
+
+// Throughput variant (2 tiles of 32 boards per wave): all 13 feature
+// fragments are built once per tile pair (104 VGPRs), then the four 32-row
+// hidden tiles m run one after another into two alternating accumulator sets;
+// the sigmoid + w2 dot product of tile m-1 is interleaved with tile m's 52
+// MFMAs (the VALU / transcendental issue fits in the MFMA gaps), so only the
+// last tile's epilogue is exposed.
+// rows r0, r0 + 1 (r0 even) of hidden tile m: w2 of j0 = 32m + (r & 3) + 8(r >> 2) + 4h
+// and j0 + 1 are adjacent in LDS (one ds_read_b64)
+BGX_DEV void epi_pair(const floatx16& acc, int m, int r0, int h, const float* w2s, float& v) {
+    const float2 c = *(const float2*)(w2s + 32 * m + (r0 & 3) + 8 * (r0 >> 2) + 4 * h);
+    const float e0 = __builtin_amdgcn_exp2f(acc[r0]), e1 = __builtin_amdgcn_exp2f(acc[r0 + 1]);
+    v = fmaf(c.x, __builtin_amdgcn_rcpf(1.0f + e0), v);
+    v = fmaf(c.y, __builtin_amdgcn_rcpf(1.0f + e1), v);
+}
+
+__global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
+    constexpr int NT = 2;
+    extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+    uint4* wf = lds;                                   // [NFRAG]
+    uint4* lut = lds + NFRAG;                          // [256]
+    float* w2s = (float*)(lds + NFRAG + 256);          // [128] value-head weights
+    for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i, a.feat_scale);
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) w2s[i] = a.rowc[i];
+
+    int n = a.n_rows;
+    if (a.n_rows_dev) n += (int)*a.n_rows_dev;
+    if (a.n_max > 0 && n > a.n_max) n = a.n_max;
+    const int tiles = (n + 32 * NT - 1) / (32 * NT);
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5;
+    const int col = lane & 31;
+    const int wave = threadIdx.x >> 6;
+    const int NW = blockDim.x >> 6;
+    const int nwaves = gridDim.x * NW;
+    __syncthreads();
+    for (int t = blockIdx.x * NW + wave; t < tiles; t += nwaves) {
+        // k-steps 0..11 from the LUT, kept in registers; k-step 12 (bars, borne-off,
+        // side to move, bias) is rebuilt from the row word per hidden tile
+        half8 b[KSTEPS - 1][NT];
+        uint32_t w6[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            uint4 bx, by;
+            load_rows(a, n, t * NT + q, NT, col, bx, by);
+#pragma unroll
+            for (int s = 0; s < KSTEPS - 1; ++s) b[s][q] = feat_frag(bx, by, s, h, lut, a.feat_scale);
+            w6[q] = by.z;
+        }
+        float v[NT] = {0.0f, 0.0f};
+        floatx16 acc[2][NT];
+        // A pair for (m, s) = (0, 0); each step loads the next pair before its MFMAs
+        uint4 ah = wf[((0 * 4 + 0) * KSTEPS + 0) * 64 + lane];
+        uint4 al = wf[((1 * 4 + 0) * KSTEPS + 0) * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int cur = m & 1, prv = cur ^ 1;
+#pragma unroll
+            for (int q = 0; q < NT; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[cur][q][r] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < KSTEPS; ++s) {
+                const int mn = s + 1 < KSTEPS ? m : (m + 1 < 4 ? m + 1 : m);
+                const int sn = s + 1 < KSTEPS ? s + 1 : 0;
+                const uint4 nh = wf[((0 * 4 + mn) * KSTEPS + sn) * 64 + lane];
+                const uint4 nl = wf[((1 * 4 + mn) * KSTEPS + sn) * 64 + lane];
+#pragma unroll
+                for (int q = 0; q < NT; ++q) {
+                    const half8 bq = s < KSTEPS - 1 ? b[s < KSTEPS - 1 ? s : 0][q]
+                                                    : feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, w6[q], 0),
+                                                                KSTEPS - 1, h, lut, a.feat_scale);
+                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, bq, acc[cur][q], 0, 0, 0);
+                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, bq, acc[cur][q], 0, 0, 0);
+                }
+                // tile m-1's epilogue, spread over k-steps 0..7 (2 rows per step per board tile)
+                if (m > 0 && s < 8) {
+#pragma unroll
+                    for (int q = 0; q < NT; ++q) epi_pair(acc[prv][q], m - 1, 2 * s, h, w2s, v[q]);
+                }
+                ah = nh;
+                al = nl;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r += 2)
+#pragma unroll
+            for (int q = 0; q < NT; ++q) epi_pair(acc[1][q], 3, r, h, w2s, v[q]);
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             v[q] += __shfl_xor(v[q], 32, 64);
@@ -238,7 +341,7 @@ __global__ __launch_bounds__(128) void value_f32_kernel(const float* __restrict_
 
 extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t stream) {
     static int n_cu = 0;
-    const int lds = bgx::NFRAG * 16 + 256 * 16;
+    const int lds = bgx::NFRAG * 16 + 256 * 16 + 128 * 4;
     if (!n_cu) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -247,6 +350,8 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
         if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds) != hipSuccess ||
             hipFuncSetAttribute((const void*)bgx::mlp_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds) != hipSuccess)
             return hipErrorInvalidValue;
     }
@@ -264,7 +369,14 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
         if (need < blocks) blocks = need;
         if (blocks <= 0) return hipSuccess;
     }
-    if (nt == 2)
+    static int il = -1;
+    if (il < 0) {
+        const char* v = getenv("BGX_MLP_IL");
+        il = v ? atoi(v) : 1;
+    }
+    if (nt == 2 && il)
+        hipLaunchKernelGGL(bgx::mlp_kernel_il, dim3(blocks), dim3(512), lds, stream, *args);
+    else if (nt == 2)
         hipLaunchKernelGGL((bgx::mlp_kernel<2, 8>), dim3(blocks), dim3(512), lds, stream, *args);
     else
         hipLaunchKernelGGL((bgx::mlp_kernel<1, 16>), dim3(blocks), dim3(1024), lds, stream, *args);
