@@ -195,6 +195,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--harvest-every", type=int, default=100)
     ap.add_argument("--two-ply-steps", type=int, default=100, help="extra 2-ply (K=4) measurement; 0 = skip")
+    ap.add_argument("--kall-steps", type=int, default=20,
+                    help="extra 2-ply K=all measurement (configs[2]: ~21 x C reply boards per decision); 0 = skip")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=7, help="mirrors src/main.py:86 (7 workers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -227,6 +229,22 @@ def main():
                                "value_rows_per_s": sum_over_ranks(d2["value_rows"], world) / el2,
                                "movegen_jobs_per_s": sum_over_ranks(d2["movegen_jobs"], world) / el2,
                                "roofline": r2, "kernels": k2}
+
+    if args.kall_steps > 0 and args.ply == 1:
+        el3, d3, tm3, d3_tm, _ = run_engine(args, world, rank, 2, 0, args.lanes, args.kall_steps, 5,
+                                            args.harvest_every, timing=True,
+                                            timing_steps=min(args.kall_steps, args.timing_steps, 10))
+        el3 = max_over_ranks(el3, world)
+        tot3 = sum_over_ranks(d3["env_steps"], world)
+        r3, k3 = roofline_for(d3_tm, tm3, "2ply")
+        r3["traffic"] = None   # the PMC passes cover the K=4 leg
+        extra["two_ply_kall"] = {"value": tot3 / el3, "unit": "env_steps/s", "steps": args.kall_steps,
+                                 "ms_per_step": el3 / args.kall_steps * 1e3,
+                                 "value_rows_per_s": sum_over_ranks(d3["value_rows"], world) / el3,
+                                 "movegen_jobs_per_s": sum_over_ranks(d3["movegen_jobs"], world) / el3,
+                                 "reply_boards_per_decision": (d3["value_rows"] - 2 * d3["env_steps"])
+                                 / max(1, d3["decisions"]),
+                                 "roofline": r3, "kernels": k3}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

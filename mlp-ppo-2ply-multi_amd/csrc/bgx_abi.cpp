@@ -459,8 +459,8 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
         int n_cu = 256;
         if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) n_cu = 256;
-        // + the slack of one partly used 512-row reservation per resident movegen wave
-        e->reply_cap = L * per_lane + n_cu * 10 * 512;
+        // + the slack of one partly used 512-row reservation per resident movegen wave (<= 32 / CU)
+        e->reply_cap = L * per_lane + n_cu * 32 * 512;
         ALLOC(e->sel, 4 * L);
         ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
         ALLOC(e->reply_V, e->reply_cap);

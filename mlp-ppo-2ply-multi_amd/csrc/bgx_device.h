@@ -118,16 +118,18 @@ BGX_DEV Root make_root(const uint32_t* w, int player) {
 BGX_DEV Node root_node(const Root& r) { return {r.m0, r.m1, r.m2, r.bar | (r.off << 4)}; }
 
 // node -> packed board words (w[0..7]) with indicator flag `flag`
+// bit i of an 8-bit value -> bit 4i (one bit per nibble)
+BGX_DEV uint32_t spread8(uint32_t x) {
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    return (x | (x << 3)) & 0x11111111u;
+}
+
 BGX_DEV void node_to_packed(const Root& r, const Node& n, uint32_t flag, uint32_t* w) {
     uint32_t hit = n.x >> 8;
-    // zero the opponent nibbles at the hit points (each was exactly 1)
-    uint32_t h0 = 0, h1 = 0, h2 = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        h0 |= ((hit >> i) & 1u) << (4 * i);
-        h1 |= ((hit >> (8 + i)) & 1u) << (4 * i);
-        h2 |= ((hit >> (16 + i)) & 1u) << (4 * i);
-    }
+    // zero the opponent nibbles at the hit points (each was exactly 1):
+    // spread each hit byte to one bit per nibble
+    const uint32_t h0 = spread8(hit & 0xFFu), h1 = spread8((hit >> 8) & 0xFFu), h2 = spread8((hit >> 16) & 0xFFu);
     uint32_t o0 = r.o0 - h0, o1 = r.o1 - h1, o2 = r.o2 - h2;
     uint32_t obar = r.obar + __popc(hit);
     uint32_t bar = n.x & 15u, off = (n.x >> 4) & 15u;

@@ -47,6 +47,7 @@ struct MovegenArgs {
     size_t ws_words_per_wave;    // >= 5 * ws_slots
     int ovf_zeroed;              // caller zeroed *ovf_count on the stream already (skip the memset)
     int heavy_t;                 // set by the launcher: doubles level size handed to the block tier
+    int exp_mode;                // development only (BGX_MG_EXP): 1 skip emission, 2 skip dedup
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
     unsigned* err_flags;
 };

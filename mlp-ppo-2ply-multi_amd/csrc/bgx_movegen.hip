@@ -57,6 +57,7 @@ struct Mem {
     uint32_t* fb;              // [F]
     uint32_t* map;             // [64] parent start marks for one child chunk (kept zero between uses)
     int S, F;
+    int exp = 0;               // development experiments (MovegenArgs::exp_mode)
 };
 
 // LDS (wavefront scope) or global (agent scope) accessors
@@ -260,6 +261,13 @@ BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
             in.d1 = a.in_dice[2 * j + 1];
         }
     }
+    // the job is wave-uniform: pin its words in SGPRs so the root analysis
+    // below (and node_moves on the root) runs on the scalar unit, not VALU
+    w0 = uniformu(w0); w1 = uniformu(w1); w2 = uniformu(w2); w3 = uniformu(w3);
+    w4 = uniformu(w4); w5 = uniformu(w5); w6 = uniformu(w6);
+    player = uniform(player);
+    in.d0 = uniform(in.d0);
+    in.d1 = uniform(in.d1);
     const bool p2 = player != 0;
     Root& R = in.R;
     R.m0 = p2 ? w3 : w0; R.m1 = p2 ? w4 : w1; R.m2 = p2 ? w5 : w2;
@@ -405,11 +413,13 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
         const uint32_t key = kfn(p, s);
         const uint32_t ord = ord_base + (uint32_t)r;
         bool fresh;
-        const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
+        uint32_t slot = 0;
+        if (M.exp & 2) fresh = act;
+        else slot = dedup_insert<G>(M, act, key, ord, fresh);
         inserted += __popcll(ballot(fresh));
         if (inserted > M.S - (M.S >> 2) || n_out + 64 > M.F) return false;
         sync<G>();
-        const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
+        const bool sv = act && ((M.exp & 2) ? true : (uint32_t)ld64<G>(M.tab + slot) == ord);
         const uint64_t bm = ballot(sv);
         if (sv) st32<G>(out + n_out + mask_prefix(bm), key | tag);
         n_out += __popcll(bm);
@@ -567,7 +577,7 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
     const int nfin = job_records<G>(in, M, fin, heavy_t);
     if (nfin < 0) return nfin;
     const int base = begin_emit(a, j, nfin, fc);
-    if (base >= 0) emit_records<G>(a, j, in, fin, nfin, base);
+    if (base >= 0 && !(M.exp & 1)) emit_records<G>(a, j, in, fin, nfin, base);
     return nfin;
 }
 
@@ -765,7 +775,8 @@ BGX_DEV void push_ovf(const MovegenArgs& a, int j) {
 template <int S>
 __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned long long smem[Slice<S>::bytes / 8];
-    const Mem M = lds_mem<S>(smem);
+    Mem M = lds_mem<S>(smem);
+    M.exp = a.exp_mode;
     const int n_jobs = uniform(job_count(a));
     FlatCursor fc;
     for (int j = (int)blockIdx.x; j < n_jobs; j += (int)gridDim.x) {
@@ -947,6 +958,7 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     }
     // test hook: route every job to tier 2 (2) or tier 3 (3)
     if (const char* v = getenv("BGX_MG_TEST_TIER")) a.force_tier = atoi(v);
+    if (const char* v = getenv("BGX_MG_EXP")) a.exp_mode = atoi(v);   // development only
     int coop = -1;
     if (const char* v = getenv("BGX_MG_COOP")) coop = atoi(v);
     // latency-bound launches (at most 4 windows of 16 jobs per CU, host-known
