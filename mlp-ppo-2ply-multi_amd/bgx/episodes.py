@@ -49,8 +49,13 @@ def decode_records(records: torch.Tensor):
 
 def to_episodes(h: Harvest, episode_cls, experience_cls, player_enum):
     """Build reference-shaped Episode objects (already in to_numpy() form)."""
-    hdr = h.headers.cpu().numpy().astype(np.uint32)
-    d = decode_records(h.records)
+    return episodes_from_arrays(h.headers.cpu().numpy().astype(np.uint32), h.records, episode_cls,
+                                experience_cls, player_enum)
+
+
+def episodes_from_arrays(hdr, records, episode_cls, experience_cls, player_enum):
+    """hdr uint32 [n, 8] (host), records int32 [m, 24] (device) -> Episodes."""
+    d = decode_records(records)
     eps = []
     o = 0
     for row in hdr:

@@ -10,11 +10,14 @@ version advances (worker.py:66-76), at every harvest.
 
 Knobs (environment): BGX_LANES (4096), BGX_PLY (1), BGX_K_TOP (4),
 BGX_STEPS_PER_HARVEST (100), BGX_MAX_PENDING (2000 episodes queued before the
-engine pauses: the queue's Python consumer is far slower than the engine).
+engine pauses: the queue's Python consumer is far slower than the engine),
+BGX_BULK (1: one shared-memory message per harvest through
+ExperienceQueue.put_records; 0: one pickled Episode per put, as the reference).
 """
 import os
 import time
 
+import numpy as np
 import torch
 
 from bgx import Engine
@@ -65,14 +68,26 @@ class Worker:
         eng.step(steps or self.steps_per_harvest)
         return to_episodes(eng.harvest(), Episode, Experience, Player)
 
+    def harvest_records(self, steps=None):
+        """Advance all lanes; return the finished episodes as compact host arrays
+        (headers uint32 [n, 8], records uint32 [m, 24]) for the bulk queue path."""
+        eng = self._ensure_engine()
+        eng.step(steps or self.steps_per_harvest)
+        h = eng.harvest()
+        return (h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32))
+
     def run(self):
         if self.device is None:
             print(f"Worker {self.worker_id}: no GPU for this worker id; idle.")
             return
         print(f"Worker {self.worker_id} starting on cuda:{self.device} with {self.lanes} lanes.")
+        bulk = hasattr(self.experience_queue, "put_records") and os.environ.get("BGX_BULK", "1") != "0"
         while True:
-            for episode in self.play_episodes():
-                self.experience_queue.put(episode)
+            if bulk:
+                self.experience_queue.put_records(*self.harvest_records())
+            else:
+                for episode in self.play_episodes():
+                    self.experience_queue.put(episode)
             self._maybe_update()
             while self.experience_queue.qsize() > self.max_pending:
                 time.sleep(0.01)

@@ -206,3 +206,34 @@ def test_graph_launch_matches_direct_launch(ply, monkeypatch):
         np.testing.assert_array_equal(a[key][0], b[key][0], err_msg=str(key))
         for f in a[key][1]:
             np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")
+
+
+def test_bulk_queue_episodes_equal_direct_path(weights_seed0):
+    """put_records -> shared-memory ring -> get() decodes (on the GPU) the same
+    Episodes as the worker-side to_episodes path."""
+    from bgx.episodes import to_episodes
+    from environments import Episode, Experience, Player
+    from multi.experience_queue import ExperienceQueue
+    e = _engine(weights_seed0, lanes=256, seed=3, ply=1)
+    e.step(150)
+    h = e.harvest()
+    direct = to_episodes(h, Episode, Experience, Player)
+    assert len(direct) > 10
+    q = ExperienceQueue(capacity_mb=64)
+    try:
+        assert q.put_records(h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32))
+        assert q.qsize() == len(direct)
+        bulk = [q.get(timeout=10) for _ in range(len(direct))]
+        assert q.qsize() == 0
+    finally:
+        q.close()
+        e.close()
+    for a, b in zip(direct, bulk):
+        assert a.win_type == b.win_type
+        assert a.close_out_counts == b.close_out_counts and a.prime_reward_counts == b.prime_reward_counts
+        assert len(a.experiences) == len(b.experiences)
+        for x, y in zip(a.experiences, b.experiences):
+            np.testing.assert_array_equal(x.observation, y.observation)
+            np.testing.assert_array_equal(x.next_observation, y.next_observation)
+            assert x.state_value == y.state_value and x.next_state_value == y.next_state_value
+            assert x.reward == y.reward and x.done == y.done
