@@ -54,24 +54,32 @@ def to_episodes(h: Harvest, episode_cls, experience_cls, player_enum):
 
 
 def episodes_from_arrays(hdr, records, episode_cls, experience_cls, player_enum):
-    """hdr uint32 [n, 8] (host), records int32 [m, 24] (device) -> Episodes."""
+    """hdr uint32 [n, 8] (host), records int32 [m, 24] (device) -> Episodes.
+    Field types follow Episode.to_numpy() (episode.py:22-46): observation
+    np.float32[198] views, state values Python floats, reward a 0-d np.float32
+    array, done bool."""
     d = decode_records(records)
+    obs, nxt = d["obs"], d["next_obs"]
+    v_s, v_a, done = d["v_s"].tolist(), d["v_a"].tolist(), d["done"].tolist()
+    rew = d["reward"].astype(np.float32).reshape(-1, 1)
+    mover, win, close, prime = d["mover"].tolist(), d["win_type"].tolist(), d["close_out"].tolist(), d["prime"].tolist()
+    players = [player_enum(0), player_enum(1)]
     eps = []
     o = 0
-    for row in hdr:
+    for row in hdr.tolist():
         n = int(row[3])
         ep = episode_cls()
         for k in range(o, o + n):
-            ex = experience_cls(observation=d["obs"][k], state_value=float(d["v_s"][k]),
-                                reward=np.array(d["reward"][k], dtype=np.float32), done=bool(d["done"][k]),
-                                next_observation=d["next_obs"][k], next_state_value=float(d["v_a"][k]))
-            info = {"current_player": player_enum(int(d["mover"][k]))}
-            if d["win_type"][k]:
-                info["win_type"] = WIN_TYPES[int(d["win_type"][k])]
-                info["winner"] = player_enum(int(d["mover"][k]))
-            if d["close_out"][k]:
+            ex = experience_cls(observation=obs[k], state_value=v_s[k], reward=rew[k].reshape(()),
+                                done=done[k], next_observation=nxt[k], next_state_value=v_a[k])
+            pl = players[mover[k]]
+            info = {"current_player": pl}
+            if win[k]:
+                info["win_type"] = WIN_TYPES[win[k]]
+                info["winner"] = pl
+            if close[k]:
                 info["close_out_reward"] = True
-            if d["prime"][k]:
+            if prime[k]:
                 info["prime_reward"] = True
             ep.add_experience(ex, info)
         o += n
