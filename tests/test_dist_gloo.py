@@ -59,3 +59,58 @@ def test_gloo_world2_broadcast_and_gather():
     tot_eps, tot_recs, lane0, tag = d["tot"]
     assert (tot_eps, tot_recs) == (1 + 2, 3 + 6)
     assert lane0 == [0, 4096] and tag == [7, 8]
+
+
+class _FakeEngine:
+    def __init__(self):
+        self.calls = []
+
+    def set_weights(self, w, temperature, version):
+        self.calls.append((float(w["b1"][0]), float(temperature), int(version)))
+
+
+def _pm_worker(rank, world, port, out):
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    from multi.parameter_manager import DistributedParameterManager
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _FakeEngine()
+    sd = {"fc1.weight": torch.zeros(128, 198), "fc1.bias": torch.full((128,), 0.5),
+          "value_head.weight": torch.ones(1, 128), "value_head.bias": torch.zeros(1)}
+    pm = DistributedParameterManager(engine=eng, src=0, state_dict=sd if rank == 0 else None)
+    first = (pm.get_version(), pm.get_temperature())
+    quiet = pm.sync()                                   # nothing new: no weight broadcast
+    if rank == 0:
+        for k in range(3):                              # three trainer updates before one sync
+            sd["fc1.bias"] = torch.full((128,), float(k + 1))
+            pm.set_parameters(sd)
+    moved = pm.sync()
+    got = pm.get_parameters()
+    out.put((rank, first, quiet, moved, pm.get_version(), pm.get_temperature(), eng.calls,
+             float(got["fc1.bias"][0]), tuple(got["value_head.weight"].shape)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_distributed_parameter_manager():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {m[0]: m[1:] for m in (q.get(timeout=120) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        first, quiet, moved, ver, temp, calls, b1, w2shape = res[r]
+        assert first == (1, 1.5)                        # version 1 everywhere after construction
+        assert quiet is False and moved is True
+        assert ver == 4 and abs(temp - (1.5 - 1.0 * 3 / 4000)) < 1e-12   # parameter_manager.py:101-111
+        assert calls == [(0.5, 1.5, 1), (3.0, temp, 4)]  # engine re-armed once per propagated version
+        assert b1 == 3.0 and w2shape == (1, 128)
