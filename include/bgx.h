@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 1
+#define BGX_ABI_VERSION 2
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -94,6 +94,8 @@ typedef struct bgx_config {
     int ep_cap;             /* finished-episode headers held between harvests */
     int cand_per_lane;      /* average candidate rows reserved per lane (1-ply buffer) */
     int reply_per_lane;     /* average 2-ply reply rows reserved per lane */
+    int greedy;             /* 1: argmax of the scores instead of sampling (play_versus_ai.py:188-195,
+                               torch.argmax: first maximum); the sampling uniform is still drawn */
 } bgx_config;
 
 void bgx_config_default(bgx_config* cfg);

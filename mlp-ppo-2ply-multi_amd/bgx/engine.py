@@ -38,7 +38,7 @@ class Harvest:
 class Engine:
     def __init__(self, lanes=4096, seed=0, ply=1, k_top=4, device=None, lane_base=0, alpha=1.0,
                  beta=0.9, max_steps=300, max_legal=500, ring=640, ep_cap=0, cand_per_lane=256,
-                 reply_per_lane=0):
+                 reply_per_lane=0, greedy=False):
         require_cuda()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         cfg = Config()
@@ -47,6 +47,7 @@ class Engine:
         cfg.ply, cfg.k_top, cfg.alpha, cfg.beta = int(ply), int(k_top), float(alpha), float(beta)
         cfg.max_steps, cfg.max_legal, cfg.ring, cfg.ep_cap = int(max_steps), int(max_legal), int(ring), int(ep_cap)
         cfg.cand_per_lane, cfg.reply_per_lane = int(cand_per_lane), int(reply_per_lane)
+        cfg.greedy = 1 if greedy else 0
         self.cfg = cfg
         self.lanes = int(lanes)
         h = ctypes.c_void_p()

@@ -147,3 +147,12 @@ class Net:
         check(lib().bgx_two_ply(self._h, ptr(boards), ptr(opponent), boards.shape[0], ptr(out),
                                 stream_handle(stream)), "bgx_two_ply")
         return out
+
+
+def load_pth(path):
+    """A reference checkpoint (torch.save of BackgammonPolicyNetwork.state_dict(),
+    parameter_manager.py:115-151: fc1.weight / fc1.bias / value_head.weight /
+    value_head.bias) -> dict of host fp32 W1, b1, w2, b2. Loaded with
+    weights_only=True (no code from the file runs)."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    return dict(zip(("W1", "b1", "w2", "b2"), weights_from(sd)))

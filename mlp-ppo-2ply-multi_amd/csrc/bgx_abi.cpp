@@ -486,6 +486,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     d.ply = cfg->ply;
     d.k_top = cfg->k_top;
     d.alpha = cfg->alpha;
+    d.greedy = cfg->greedy != 0;
     d.beta = cfg->beta;
     d.rows = e->rows;
     d.cand_cap = e->cand_cap;

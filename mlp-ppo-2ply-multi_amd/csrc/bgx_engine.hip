@@ -304,10 +304,25 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
     for (int k = l; k < m; k += 64) sum += __expf(x[k] - mx);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    int pick = m - 1;
+    if (e.greedy) {
+        // argmax, first maximum (torch.argmax; the temperature does not change it)
+        float bv = -INFINITY;
+        int bk = 0x7FFFFFFF;
+        for (int k = l; k < m; k += 64)
+            if (x[k] > bv) { bv = x[k]; bk = k; }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float ov = __shfl_xor(bv, off, 64);
+            const int ok = __shfl_xor(bk, off, 64);
+            if (ov > bv || (ov == bv && ok < bk)) { bv = ov; bk = ok; }
+        }
+        if (l == 0) step_lane(e, i, k4 ? e.sel[4 * i + bk] - base : bk);
+        return;
+    }
     const uint64_t key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
     const float u = unit_from(philox(key, 0x5EED0000ull, e.rng[i]).x);
     const float t = u * sum;
-    int pick = m - 1;
     float carry = 0.0f;
     for (int b = 0; b < m; b += 64) {
         const int k = b + l;

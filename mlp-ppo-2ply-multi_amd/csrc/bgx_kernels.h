@@ -80,6 +80,7 @@ struct EngineDev {
     int ply;                     // 1 or 2
     int k_top;                   // 4 (two_ply.py:67-70) or 0 = all candidates
     float alpha, beta;           // 1.0, 0.9 (two_ply.py:44-50)
+    int greedy;                  // argmax instead of sampling (play_versus_ai.py:188-195)
     uint32_t* rows;              // [L + cand_cap][8]: lane boards (obs rows) then candidates
     int cand_cap;
     uint8_t* player;             // [L]

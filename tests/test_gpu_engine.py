@@ -237,3 +237,23 @@ def test_bulk_queue_episodes_equal_direct_path(weights_seed0):
             np.testing.assert_array_equal(x.next_observation, y.next_observation)
             assert x.state_value == y.state_value and x.next_state_value == y.next_state_value
             assert x.reward == y.reward and x.done == y.done
+
+
+def test_engine_greedy_picks_the_highest_value(weights_ckpt):
+    """greedy=True (play_versus_ai.py:188-195): the chosen afterstate has the
+    largest V among the legal candidates (within the V tolerance), checked
+    against the oracle's fp64 values on the shipped checkpoint."""
+    e = _engine(weights_ckpt, lanes=128, seed=21, ply=1, greedy=True)
+    hdrs, recs = _collect(e, 150, chunk=50)
+    e.close()
+    n = 0
+    for d in recs:
+        for k in range(len(d["action"])):
+            b, mover, dice = d["before"][k], int(d["mover"][k]), d["dice"][k]
+            cnt, res, _ = orc.movegen(b, mover, int(dice[0]), int(dice[1]))
+            m = min(cnt, 500)
+            v = orc.value(weights_ckpt, orc.encode_many(res[:m], [mover] * m))
+            a = int(d["action"][k])
+            assert v[a] >= v.max() - V_TOL, (k, a, v[a], v.max())
+            n += 1
+    assert n > 2000

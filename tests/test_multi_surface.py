@@ -66,3 +66,21 @@ def test_experience_queue_roundtrip():
     assert isinstance(got, Episode)
     with pytest.raises(queue.Empty):
         q.get(timeout=0.05)
+
+
+def test_load_pth_round_trip(tmp_path):
+    """A reference-format checkpoint (state_dict of BackgammonPolicyNetwork,
+    parameter_manager.py:115-151) loads through bgx.ops.load_pth (weights_only)."""
+    import torch
+    from bgx.net import BackgammonPolicyNetwork
+    from bgx.ops import load_pth
+    torch.manual_seed(3)
+    net = BackgammonPolicyNetwork()
+    p = tmp_path / "ppo_backgammon.pth"
+    torch.save(net.state_dict(), p)
+    w = load_pth(str(p))
+    sd = net.state_dict()
+    np.testing.assert_array_equal(w["W1"], sd["fc1.weight"].numpy())
+    np.testing.assert_array_equal(w["b1"], sd["fc1.bias"].numpy())
+    np.testing.assert_array_equal(w["w2"], sd["value_head.weight"].numpy().reshape(128))
+    np.testing.assert_array_equal(w["b2"], sd["value_head.bias"].numpy())
