@@ -1,0 +1,139 @@
+"""TD(0) trainer on device-resident episodes.
+
+The reference's consumer (src/agents/trainer.py:10-166, Trainer.update) takes
+exactly MIN_EPISODES_TO_TRAIN = 200 Episodes and, for each episode in turn:
+Y = V(observations) (trainer.py:106-107), target = rewards with
+gamma * Y[1:].detach() added to all but the last step (110-114), MSE loss
+(117), zero_grad / backward (120-121), clip_grad_norm_(params, 1.0) (124-127),
+the post-clip gradient norm as a metric (130-135), Adam step (lr 1e-3; the
+configured LR decay is never applied in the reference) (138), then the new
+state_dict goes to the ParameterManager (161).
+
+DeviceTrainer.update_records() runs the same per-episode sequence straight
+from the engine's compact records (the observations are re-encoded on the
+GPU with bgx_encode; no Python Episode objects), and update(episodes) keeps
+the reference's signature. batched=True is a flagged semantic change: one
+Adam step per update on the mean of the per-episode losses.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .engine import WIN_TYPES
+from .net import BackgammonPolicyNetwork
+
+LEARNING_RATE = 1e-3          # config/configuration.py:17
+GAMMA = 0.99                  # configuration.py:15
+GRAD_CLIP_THRESHOLD = 1.0     # configuration.py:18
+MIN_EPISODES_TO_TRAIN = 200   # configuration.py:7
+
+
+class DeviceTrainer:
+    def __init__(self, parameter_manager, device=None, lr=LEARNING_RATE, gamma=GAMMA,
+                 grad_clip=GRAD_CLIP_THRESHOLD, batch_episode_size=MIN_EPISODES_TO_TRAIN, batched=False):
+        self.parameter_manager = parameter_manager
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.policy_network = BackgammonPolicyNetwork().to(self.device)
+        sd = {k: torch.as_tensor(v).to(self.device) for k, v in parameter_manager.get_parameters().items()}
+        self.policy_network.load_state_dict(sd)
+        self.optimizer = torch.optim.Adam(self.policy_network.parameters(), lr=lr)
+        self.gamma = torch.tensor(gamma, device=self.device)
+        self.grad_clip = grad_clip
+        self.batch_episode_size = batch_episode_size
+        self.batched = batched
+        self.total_episodes = 0
+
+    # ------------------------------------------------------------ inputs
+    def _from_records(self, headers, records):
+        """(observations [m, 198], rewards [m], episode lengths, win types) on the device."""
+        rec = torch.as_tensor(records).to(self.device)
+        if rec.dtype != torch.int32:
+            rec = rec.view(torch.int32) if rec.dtype == torch.uint32 else rec.to(torch.int32)
+        before = rec[:, 0:8].contiguous()
+        obs = ops.encode(ops.unpack(before), ops.packed_player(before))
+        rewards = rec[:, 18].contiguous().view(torch.float32)
+        hdr = np.asarray(torch.as_tensor(headers).cpu().numpy()).astype(np.uint32)
+        lens = hdr[:, 3].astype(np.int64).tolist()
+        wins = [WIN_TYPES[int(w) & 0xFF] for w in (hdr[:, 5] & 0xFF).tolist()]
+        return obs, rewards, lens, wins
+
+    def _from_episodes(self, episodes):
+        obs, rew, lens, wins = [], [], [], []
+        for ep in episodes:
+            obs.extend(torch.as_tensor(np.asarray(x.observation, np.float32)) for x in ep.experiences)
+            rew.extend(float(np.asarray(x.reward)) for x in ep.experiences)
+            lens.append(len(ep.experiences))
+            wins.append(ep.win_type)
+        obs_t = torch.stack(obs).to(self.device) if obs else torch.zeros((0, 198), device=self.device)
+        return obs_t, torch.tensor(rew, dtype=torch.float32, device=self.device), lens, wins
+
+    # ------------------------------------------------------------ update
+    def update(self, episodes):
+        """Trainer.update(episodes) (trainer.py:49-166): exactly batch_episode_size episodes."""
+        if len(episodes) != self.batch_episode_size:
+            raise ValueError(f"Expected {self.batch_episode_size} episodes, but got {len(episodes)}.")
+        return self._update(*self._from_episodes(episodes))
+
+    def update_records(self, headers, records):
+        """The same update from compact records (headers [n, 8], records [m, 24],
+        each episode's records contiguous in header order); any n >= 1."""
+        return self._update(*self._from_records(headers, records))
+
+    def _update(self, obs, rewards, lens, wins):
+        net, opt = self.policy_network, self.optimizer
+        params = list(net.parameters())
+        n_eps = len(lens)
+        self.total_episodes += n_eps
+        m = {"loss": 0.0, "td_error": 0.0, "grad_norm": 0.0, "predicted_value": 0.0, "reward": 0.0,
+             "episode_length": 0.0}
+        win_counts = {"regular": 0, "gammon": 0, "backgammon": 0}
+        offs = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        if self.batched:
+            losses = []
+            for e in range(n_eps):
+                y, tgt = self._episode_terms(obs, rewards, offs[e], offs[e + 1])
+                losses.append(F.mse_loss(y, tgt))
+            opt.zero_grad()
+            loss = torch.stack(losses).mean()
+            loss.backward()
+            if self.grad_clip is not None:
+                torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
+            opt.step()
+            m["loss"] = float(loss) * n_eps
+        else:
+            for e in range(n_eps):
+                y, tgt = self._episode_terms(obs, rewards, offs[e], offs[e + 1])
+                loss = F.mse_loss(y, tgt)
+                opt.zero_grad()
+                loss.backward()
+                if self.grad_clip is not None:
+                    torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
+                gn = 0.0
+                for p in params:
+                    if p.grad is not None:
+                        gn += p.grad.data.norm(2).item() ** 2
+                m["grad_norm"] += gn ** 0.5
+                opt.step()
+                m["td_error"] += (tgt - y).abs().mean().item()
+                m["loss"] += loss.item()
+                m["predicted_value"] += y.mean().item()
+                m["reward"] += rewards[offs[e]:offs[e + 1]].sum().item()
+                m["episode_length"] += offs[e + 1] - offs[e]
+        for w in wins:
+            if w in win_counts:
+                win_counts[w] += 1
+        self.parameter_manager.set_parameters(net.state_dict())
+        out = {k: v / max(1, n_eps) for k, v in m.items()}
+        out["win_counts"] = win_counts
+        out["episodes"] = n_eps
+        return out
+
+    def _episode_terms(self, obs, rewards, a, b):
+        y = self.policy_network(obs[a:b]).squeeze()
+        tgt = rewards[a:b].clone().squeeze()
+        if b - a > 1:
+            tgt[:-1] += self.gamma * y[1:].detach()
+        return y, tgt
