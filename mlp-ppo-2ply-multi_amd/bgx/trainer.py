@@ -91,6 +91,8 @@ class DeviceTrainer:
              "episode_length": 0.0}
         win_counts = {"regular": 0, "gammon": 0, "backgammon": 0}
         offs = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        # metrics accumulate on the device; one host read per update
+        acc = torch.zeros(6, dtype=torch.float64, device=self.device)
         if self.batched:
             losses = []
             for e in range(n_eps):
@@ -102,7 +104,7 @@ class DeviceTrainer:
             if self.grad_clip is not None:
                 torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
             opt.step()
-            m["loss"] = float(loss) * n_eps
+            acc[0] = loss.detach() * n_eps
         else:
             for e in range(n_eps):
                 y, tgt = self._episode_terms(obs, rewards, offs[e], offs[e + 1])
@@ -110,18 +112,20 @@ class DeviceTrainer:
                 opt.zero_grad()
                 loss.backward()
                 if self.grad_clip is not None:
-                    torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
-                gn = 0.0
-                for p in params:
-                    if p.grad is not None:
-                        gn += p.grad.data.norm(2).item() ** 2
-                m["grad_norm"] += gn ** 0.5
+                    pre = torch.nn.utils.clip_grad_norm_(params, self.grad_clip)
+                    # the reference measures the norm after clipping (trainer.py:130-135):
+                    # torch scales by min(1, clip / (norm + 1e-6))
+                    post = pre * torch.clamp(self.grad_clip / (pre + 1e-6), max=1.0)
+                else:
+                    post = torch.norm(torch.stack([p.grad.detach().norm(2) for p in params if p.grad is not None]), 2)
                 opt.step()
-                m["td_error"] += (tgt - y).abs().mean().item()
-                m["loss"] += loss.item()
-                m["predicted_value"] += y.mean().item()
-                m["reward"] += rewards[offs[e]:offs[e + 1]].sum().item()
-                m["episode_length"] += offs[e + 1] - offs[e]
+                yd = y.detach()
+                acc += torch.stack([loss.detach().double(), post.double(), (tgt - yd).abs().mean().double(),
+                                    yd.mean().double(), rewards[offs[e]:offs[e + 1]].sum().double(),
+                                    torch.zeros((), dtype=torch.float64, device=self.device)])
+        a = acc.tolist()
+        m["loss"], m["grad_norm"], m["td_error"], m["predicted_value"], m["reward"] = a[0], a[1], a[2], a[3], a[4]
+        m["episode_length"] = float(offs[-1])
         for w in wins:
             if w in win_counts:
                 win_counts[w] += 1
