@@ -170,6 +170,48 @@ BGX_DEV Node rebuild(const Root& R, uint32_t key, int d) {
     return n;
 }
 
+// ---- doubles without a table (first-reach paths only) ----------------------
+// Outside bear-off a node's move list is its movable sources in ascending
+// position (bar entry alone while on the bar), so the first-reach path of a
+// board (the lexicographically smallest index sequence, which the reference's
+// DFS records) takes, at every step, the lowest source movable there. A path
+// is first-reach iff no later step uses a source that was movable, and lower,
+// at an earlier step. Keeping only such paths gives every board once, already
+// in first-reach order: no hash table, no dedup, no duplicate children.
+// Valid when no node of the tree can be in bear-off (>= 5 mover checkers
+// outside home, bar included); other jobs take the table path.
+constexpr uint32_t PATHF = 0x40000000u;        // frontier / record entry is a path
+constexpr uint32_t PATH_EMPTY = KEY_EMPTY4;   // four empty 5-bit fields
+
+BGX_DEV bool doubles_by_path(const Root& R) {
+    const uint32_t home = R.player == 0 ? nibsum(R.m2 >> 8) : nibsum(R.m0 & 0xFFFFFFu);
+    return 15u - R.off - home >= 5u;   // outside home (points and bar)
+}
+// node after the path's steps (abs sources, in order) and the sources the
+// path rules out: movable at an earlier step and below that step's source
+BGX_DEV Node path_node(const Root& R, uint32_t path, int d, uint32_t okd, uint32_t& bad) {
+    Node n = root_node(R);
+    bad = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t f = (path >> (5 * i)) & 31u;
+        if (f != 31u) {
+            if (f < 24u) bad |= occ24(n.m0, n.m1, n.m2) & okd & ((1u << f) - 1u);
+            n = apply_move(R, n, (int)f, d);
+        }
+    }
+    return n;
+}
+BGX_DEV Node path_board(const Root& R, uint32_t path, int d) {
+    Node n = root_node(R);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t f = (path >> (5 * i)) & 31u;
+        if (f != 31u) n = apply_move(R, n, (int)f, d);
+    }
+    return n;
+}
+
 // non-doubles: positions 0..23 points, 24 = BAR (source), 25 = OFF (dest), 31 = none
 BGX_DEV int dest_of(const Root& R, int s, int d) {
     const int t = s == 24 ? (R.player == 0 ? d - 1 : 24 - d) : (R.player == 0 ? s + d : s - d);
@@ -368,6 +410,9 @@ BGX_DEV int select_bit_fast(uint32_t m, int j) {
     return base + __ffs(m) - 1;
 }
 
+// would appending T entries at n overflow a list of F?
+BGX_DEV bool n_out_check(int n, int T, int F) { return n + T > F; }
+
 // Parent lane of child r = b + lane in a flat enumeration: the last lane q
 // with c > 0 and excl <= r. Parents starting inside [b, b + 64) mark
 // map[excl - b] = q + 1; a max-scan over the marks fills the gaps; before the
@@ -506,6 +551,72 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         const uint32_t okd = ok_mask(R.block, d, R.player);
         uint32_t* fa = M.fa;
         uint32_t* fb = M.fb;
+        if (doubles_by_path(R)) {
+            if (l == 0) st32<G>(fa, PATH_EMPTY);
+            sync<G>();
+            int n = 1, level = 0;
+            while (level < 4) {
+                int nn = 0;
+                uint32_t T = 0;
+                for (int b = 0; b < n; b += 64) {
+                    const int i = b + l;
+                    const bool live = i < n;
+                    const uint32_t path = live ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
+                    uint32_t bad;
+                    const Node nd = path_node(R, path, d, okd, bad);
+                    Moves pm = node_moves(R, nd, d, okd);
+                    const uint32_t one = pm.n == 1 ? FLAG1 : 0u;
+                    pm.src &= ~bad;                      // e0 is the bar entry (or none) here
+                    pm.nsrc = __popc(pm.src);
+                    const int c = live ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0;
+                    const int incl = wave_incl_scan(c);
+                    const int excl = incl - c;
+                    const int Tc = lane63(incl);
+                    if (n_out_check(nn, Tc, M.F)) return -1;
+                    for (int cb = 0; cb < Tc; cb += 64) {
+                        const int r = cb + l;
+                        const int p = flat_parent<G>(M.map, excl, c, cb);
+                        const int jj = r - __shfl(excl, p, 64);
+                        const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+                        const int nsrc = __shfl(pm.nsrc, p, 64);
+                        const int e0 = __shfl(pm.e0, p, 64);
+                        const uint32_t pp = (uint32_t)__shfl((int)path, p, 64);
+                        const uint32_t tag = (uint32_t)__shfl((int)one, p, 64);
+                        const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
+                        // append the step in the first empty field (level)
+                        const uint32_t child = (pp & ~(31u << (5 * level))) | ((uint32_t)sx << (5 * level));
+                        if (r < Tc) st32<G>(fb + nn + r, child | tag | PATHF);
+                    }
+                    nn += Tc;
+                    T += (uint32_t)Tc;
+                    if ((int)T > heavy_t) return -2;
+                }
+                sync<G>();
+                if (T == 0) break;
+                uint32_t* t = fa; fa = fb; fb = t;
+                n = nn;
+                ++level;
+            }
+            fin = fa;
+            if (level == 0) {
+                nfin = 0;
+            } else if (level == 4) {
+                nfin = n;
+            } else {
+                for (int b = 0; b < n; b += 64) {   // parent had one move (order kept)
+                    const int i = b + l;
+                    const uint32_t e = i < n ? ld32<G>(fa + i) : 0u;
+                    const bool rec = i < n && (e & FLAG1);
+                    const uint64_t bm = ballot(rec);
+                    sync<G>();
+                    if (rec) st32<G>(fa + nfin + mask_prefix(bm), e);
+                    nfin += __popcll(bm);
+                    sync<G>();
+                }
+            }
+            fin_out = fin;
+            return nfin;
+        }
         if (l == 0) st32<G>(fa, KEY_EMPTY4);
         sync<G>();
         int n = 1, level = 0;
@@ -564,7 +675,8 @@ BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const ui
         const int i = b + lane_id();
         if (i < nfin) {
             const uint32_t e = ld32<G>(fin + i);
-            const Node n = dbl ? rebuild(in.R, e & KEYMASK, in.d0) : nd_board(in.R, e);
+            const Node n = !dbl ? nd_board(in.R, e)
+                                : ((e & PATHF) ? path_board(in.R, e & KEYMASK, in.d0) : rebuild(in.R, e & KEYMASK, in.d0));
             emit_one(a, j, in.R, n, i, base);
         }
     }
