@@ -741,8 +741,86 @@ BGX_DEV int block_excl_scan(CoopLds& C, int v, int& total) {
     return before + incl - v;
 }
 
+// The table-free path expansion (doubles_by_path) by a whole block: per level
+// the parents' filtered move lists and child prefix, then one child per
+// thread written straight to its first-reach slot (no dedup, no ranking).
+BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
+    const Root& R = in.R;
+    const int d = in.d0;
+    const int t = (int)threadIdx.x, w = t >> 6;
+    const uint32_t okd = ok_mask(R.block, d, R.player);
+    uint32_t* fa = C.fa;
+    uint32_t* fb = C.fb;
+    if (t == 0) fa[0] = PATH_EMPTY;
+    __syncthreads();
+    int n = 1, level = 0;
+    while (level < 4) {
+        int c[2] = {0, 0};
+        uint32_t src[2] = {0u, 0u}, pack[2] = {0u, 0u};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            if (hh * NTH + 64 * w < n) {        // wave-uniform
+                const int i = hh * NTH + t;
+                const uint32_t path = i < n ? fa[i] & KEYMASK : PATH_EMPTY;
+                uint32_t bad;
+                const Moves pm = node_moves(R, path_node(R, path, d, okd, bad), d, okd);
+                const uint32_t ok = pm.src & ~bad;
+                const int ns = __popc(ok);
+                c[hh] = i < n ? ns + (pm.e0 >= 0 ? 1 : 0) : 0;
+                src[hh] = ok;
+                pack[hh] = (uint32_t)ns | ((uint32_t)(pm.e0 + 1) << 5) | (pm.n == 1 ? 1u << 15 : 0u);
+            }
+        }
+        int tot2;
+        const int ex2 = block_excl_scan(C, c[0] | (c[1] << 16), tot2);
+        const int T0 = tot2 & 0xFFFF, T = T0 + (tot2 >> 16);
+        if (T == 0) break;                      // uniform
+        if (T > K_F) return -1;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int i = hh * NTH + t;
+            if (i < n) {
+                const int ex = hh ? T0 + (ex2 >> 16) : (ex2 & 0xFFFF);
+                C.psrc[i] = src[hh];
+                C.ppack[i] = pack[hh];
+                C.pexcl[i] = (uint32_t)ex;
+                for (int k = 0; k < c[hh]; ++k) C.map[ex + k] = (uint16_t)i;
+            }
+        }
+        __syncthreads();
+        for (int r = t; r < T; r += NTH) {
+            const int p = (int)C.map[r];
+            const uint32_t pk = C.ppack[p];
+            const int jj = r - (int)C.pexcl[p];
+            const int nsrc = (int)(pk & 31u);
+            const int sx = jj < nsrc ? select_bit_fast(C.psrc[p], jj) : (int)((pk >> 5) & 31u) - 1;
+            const uint32_t pp = fa[p] & KEYMASK;
+            const uint32_t child = (pp & ~(31u << (5 * level))) | ((uint32_t)sx << (5 * level));
+            fb[r] = child | (((pk >> 15) & 1u) ? FLAG1 : 0u) | PATHF;
+        }
+        __syncthreads();
+        uint32_t* tmp = fa; fa = fb; fb = tmp;
+        n = T;
+        ++level;
+    }
+    fin = fa;
+    if (level == 4) return n;
+    if (level == 0) return 0;
+    const int i0 = 2 * t;
+    const uint32_t e0 = i0 < n ? fa[i0] : 0u, e1 = i0 + 1 < n ? fa[i0 + 1] : 0u;
+    const int f0 = (i0 < n && (e0 & FLAG1)) ? 1 : 0, f1 = (i0 + 1 < n && (e1 & FLAG1)) ? 1 : 0;
+    int nf;
+    const int pos = block_excl_scan(C, f0 + f1, nf);
+    if (f0) fb[pos] = e0;
+    if (f1) fb[pos + f0] = e1;
+    __syncthreads();
+    fin = fb;
+    return nf;
+}
+
 // returns the record count (records in `fin`), -1 = overflow (tier 3)
 BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin) {
+    if (doubles_by_path(in.R)) return coop_doubles_path(in, C, fin);
     const Root& R = in.R;
     const int d = in.d0;
     const int t = (int)threadIdx.x, l = lane_id();
@@ -1034,7 +1112,9 @@ __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
         if (base >= 0) {
             for (int i = (int)threadIdx.x; i < nfin; i += NTH) {
                 const uint32_t e = fin[i];
-                emit_one(a, j, in.R, rebuild(in.R, e & KEYMASK, in.d0), i, base);
+                emit_one(a, j, in.R,
+                         (e & PATHF) ? path_board(in.R, e & KEYMASK, in.d0) : rebuild(in.R, e & KEYMASK, in.d0),
+                         i, base);
             }
         }
         __syncthreads();
