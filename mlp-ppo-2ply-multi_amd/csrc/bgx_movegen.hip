@@ -1164,7 +1164,11 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     if (const char* v = getenv("BGX_MG_HEAVY_T")) heavy = atoi(v);
     // heavy doubles go to the block-cooperative tier 2 when the launch is
     // latency-bound (BGX_MG_COOP=1/0 forces it on/off)
-    a.heavy_t = (coop == 1 || (coop < 0 && few_jobs)) ? heavy : 0x7FFFFFFF;
+    // heavy-doubles hand-off to tier 2: off by default since doubles outside
+    // bear-off expand table-free in tier 1 (measured 1-ply: off 66-67 M env
+    // steps/s, thresholds 32 / 64 / 128 / 256: 53 / 61-64 / 60 / 57 M)
+    (void)few_jobs;
+    a.heavy_t = coop == 1 ? heavy : 0x7FFFFFFF;
     if (few) {
         int blocks = a.n_jobs_dev ? n_cu * per_cuf : (a.n_jobs + bgx::BW - 1) / bgx::BW;
         if (blocks > n_cu * per_cuf) blocks = n_cu * per_cuf;
