@@ -228,6 +228,47 @@ BGX_DEV uint32_t nd_key(uint32_t s1, uint32_t t1, bool h1, uint32_t s2, uint32_t
     const uint32_t hh0 = h1 ? t1 : 31u, hh1 = h2 ? t2 : 31u;
     return sort2(r0, r1) | (sort2(a0, a1) << 10) | (sort2(hh0, hh1) << 20);
 }
+
+// Non-doubles without a table. With nothing on the bar and >= 3 mover
+// checkers outside home no node of the two-step tree is in bear-off, and the
+// 2-move plays enumerated in (pass, i, j) order (pass 0: high die first) fall
+// into two kinds:
+//  - two checkers (no step lands on the other's source): the pass-0 play
+//    (a with H, b with L) is the only pass-0 producer of its board and its
+//    pass-1 twin (b with L, a with H) is always legal: keep pass 0 only;
+//  - one checker x moving H + L: producers A = pass-0 chain x -> x+H -> .,
+//    B = pass-0 reverse (x+L with H, then x with L; x+L mover-occupied),
+//    C = pass-1 chain x -> x+L -> ., D = pass-1 reverse (x+H with L, then x
+//    with H). A chain that hits at its intermediate point makes a board no
+//    other play makes; the others make the same board and the first legal one
+//    in enumeration order (ascending first source within a pass) is kept.
+// This reproduces first-occurrence dedup (handle_non_doubles,
+// generate_all_moves.py:28-68) exactly on those positions; others use the table.
+constexpr uint32_t ND_DROP = 0xFFFFFFFFu;
+BGX_DEV bool nd_by_rule(const Root& R) {
+    const uint32_t home = R.player == 0 ? nibsum(R.m2 >> 8) : nibsum(R.m0 & 0xFFFFFFu);
+    return R.bar == 0u && 15u - R.off - home >= 3u;
+}
+BGX_DEV bool nd_first(const Root& R, uint32_t occ0, int pass, int s1, int t1, int s2, int t2, int H, int L) {
+    const bool chain = s2 == t1;
+    if (!chain && t2 != s1) return pass == 0;
+    if (chain && ((R.blot >> t1) & 1u)) return true;
+    const int x = chain ? s1 : s2;
+    const int iH = R.player == 0 ? x + H : x - H, iL = R.player == 0 ? x + L : x - L;
+    const uint32_t bad = R.block | R.blot;
+    const bool A = !((bad >> iH) & 1u), B = (occ0 >> iL) & 1u;
+    const bool C = !((bad >> iL) & 1u), D = (occ0 >> iH) & 1u;
+    // rank in enumeration order: player 0 (sources ascend with travel) A B C D,
+    // player 1 B A D C
+    const int me = pass == 0 ? (chain ? 0 : 1) : (chain ? 2 : 3);
+    const bool p0 = R.player == 0;
+    switch (me) {
+        case 0: return p0 ? true : !B;
+        case 1: return p0 ? !A : true;
+        case 2: return !A && !B && (p0 ? true : !D);
+        default: return !A && !B && (p0 ? !C : true);
+    }
+}
 BGX_DEV void nib_add(Node& n, int p, int delta) {
     const uint32_t v = 1u << ((p & 7) * 4);
     const int w = p >> 3;
@@ -473,6 +514,32 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
     return true;
 }
 
+// expand_flat without a table: kfn returns ND_DROP for children that an
+// earlier child already produced (nd_first); the rest are appended in order
+template <bool G, typename KeyFn>
+BGX_DEV bool expand_keep(const Mem& M, const Moves& pm, int c, KeyFn kfn, uint32_t* out, int& n_out) {
+    const int l = lane_id();
+    const int incl = wave_incl_scan(c);
+    const int excl = incl - c;
+    const int T = lane63(incl);
+    for (int b = 0; b < T; b += 64) {
+        const int r = b + l;
+        const int p = flat_parent<G>(M.map, excl, c, b);
+        const int j = r - __shfl(excl, p, 64);
+        const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+        // kfn shuffles from the parent lane: every lane runs it (a lane
+        // masked off by a branch returns nothing to ds_bpermute)
+        const uint32_t key = kfn(p, select_bit_fast(src, j));
+        const bool sv = r < T && key != ND_DROP;
+        const uint64_t bm = ballot(sv);
+        if (n_out + 64 > M.F) return false;
+        if (sv) st32<G>(out + n_out + mask_prefix(bm), key);
+        n_out += __popcll(bm);
+    }
+    sync<G>();
+    return true;
+}
+
 // ------------------------------------------------------------------ the job
 // returns the record count, or -1 when the slice overflowed (fallback)
 // heavy_t: a doubles level with more children than this returns -2 (the
@@ -506,16 +573,40 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         int s1 = 0;
         if (v1) s1 = move_source(mA, k);
         const Node child = v1 ? apply_move(R, root, s1, dA) : root;
-        const Moves m2 = node_moves(R, child, dB, pass ? okH : okL);
+        Moves m2 = node_moves(R, child, dB, pass ? okH : okL);
         const int c = v1 ? m2.n : 0;
         const bool two1 = ballot(in32 && pass == 0 && c > 0) != 0ull;
         const bool two2 = ballot(in32 && pass == 1 && c > 0) != 0ull;
         const int nH = mH.n, nL = mL.n;
-        clear_tab<G>(M);
         const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
         const bool h1 = v1 && t1 < 24u && ((R.blot >> t1) & 1u);
-        if (two1 || (nH != 1 && two2)) {
+        if ((two1 || (nH != 1 && two2)) && nd_by_rule(R) && !(M.exp & 4)) {
+            // 2-move records without a table (nd_first): a pass-2 parent can
+            // only add its chain (s2 = t1) or reverse chain (s2 -> s1) child
+            if (pass == 1) {
+                const int rv = R.player == 0 ? s1 - H : s1 + H;
+                const uint32_t cand = (t1 < 24u ? 1u << t1 : 0u) | ((rv >= 0 && rv < 24) ? 1u << rv : 0u);
+                m2.src &= cand;
+                m2.nsrc = m2.n = __popc(m2.src);
+            }
+            const int cc = v1 ? m2.n : 0;
+            const uint32_t blot2 = R.blot & ~(h1 ? (1u << t1) : 0u);
+            const uint32_t occ0 = occ24(R.m0, R.m1, R.m2);
+            auto kfn = [&](int p, int s2) -> uint32_t {
+                const int ps1 = __shfl(s1, p, 64);
+                const int pt1 = __shfl((int)t1, p, 64);
+                const uint32_t pb2 = (uint32_t)__shfl((int)blot2, p, 64);
+                const bool ph1 = __shfl((int)h1, p, 64) != 0;
+                const int pp = p >> 4;
+                const int t2 = dest_of(R, s2, pp ? H : L);
+                const bool h2 = ((pb2 >> t2) & 1u) != 0u;
+                const uint32_t key = nd_key((uint32_t)ps1, (uint32_t)pt1, ph1, (uint32_t)s2, (uint32_t)t2, h2);
+                return nd_first(R, occ0, pp, ps1, pt1, s2, t2, H, L) ? key : ND_DROP;
+            };
+            if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin)) return -1;
+        } else if (two1 || (nH != 1 && two2)) {
             // 2-move records in (pass, i, j) order (handle_non_doubles 43-68, both passes)
+            clear_tab<G>(M);
             const int cc = in32 ? c : 0;
             const uint32_t blot2 = R.blot & ~(h1 ? (1u << t1) : 0u);
             auto kfn = [&](int p, int s2) -> uint32_t {
@@ -533,6 +624,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         } else {
             // singles: high-die singles, then (unless pass 2 is skipped) low-die singles
             // (handle_non_doubles 70-81; generate_all_moves.py:40-50)
+            clear_tab<G>(M);
             const int nL2 = (nH == 1) ? 0 : nL;
             const bool act = v1 && (pass == 0 || k < nL2);
             const uint32_t ord = pass == 0 ? (uint32_t)k : (uint32_t)(nH + k);

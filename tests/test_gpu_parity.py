@@ -110,6 +110,49 @@ def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, few, coop, monkeypatch):
             np.testing.assert_array_equal(out[i, :n], res, err_msg=f"job {s + i}")
 
 
+def _random_positions(seed, n):
+    """Checkers dropped uniformly on the points (the two sides on disjoint
+    points), a few on the bar or borne off: adjacent blots, stacks and
+    reverse chains far more often than self-play reaches them."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        b = np.zeros(52, np.uint8)
+        pts = rng.permutation(24)
+        k = int(rng.integers(2, 12))
+        side = [pts[:k], pts[k:k + int(rng.integers(2, 24 - k))]]
+        for pl in (0, 1):
+            left = 15
+            off = int(rng.choice([0, 0, 0, int(rng.integers(0, 6))]))
+            bar = int(rng.choice([0, 0, 0, 0, 1, 2]))
+            b[50 + pl], b[48 + pl] = off, bar
+            left -= off + bar
+            for _c in range(left):
+                b[24 * pl + int(rng.choice(side[pl]))] += 1
+        out.append((b, int(rng.integers(0, 2))))
+    return out
+
+
+@pytest.mark.parametrize("rule", ["0", "4"])
+def test_movegen_random_positions_vs_oracle(bgx_ops, rule, monkeypatch):
+    """Random placements, all 36 rolls; non-doubles by the table-free rule
+    (default) and with it disabled (BGX_MG_EXP=4)."""
+    monkeypatch.setenv("BGX_MG_EXP", rule)
+    pos = _random_positions(99, 1500)
+    rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
+    boards = np.stack([p[0] for p in pos for _ in rolls])
+    player = np.array([p[1] for p in pos for _ in rolls], np.uint8)
+    dice = np.array([r for _ in pos for r in rolls], np.uint8)
+    cap = 1024
+    for s in range(0, len(boards), 8192):
+        e = min(len(boards), s + 8192)
+        out, cnt = _run_movegen(bgx_ops, boards[s:e], player[s:e], dice[s:e], cap)
+        for i in range(e - s):
+            n, res, _ = orc.movegen(boards[s + i], player[s + i], *dice[s + i], cap=cap)
+            assert cnt[i] == n, (s + i, cnt[i], n)
+            np.testing.assert_array_equal(out[i, :n], res, err_msg=f"job {s + i}")
+
+
 def test_movegen_zero_and_empty(bgx_ops):
     out, cnt = bgx_ops.movegen(torch.zeros((0, 52), dtype=torch.uint8).cuda(),
                                torch.zeros((0,), dtype=torch.uint8).cuda(),
