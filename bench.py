@@ -33,6 +33,8 @@ FP16_DENSE_PEAK_TFS = 2500.0  # dense fp16 MFMA (no sparsity)
 MLP_FLOP_PER_ROW = 50944     # 2 * (198*128 + 128)  
 MOVEGEN_BYTES_PER_JOB = 54   # parent board + player + dice
 MOVEGEN_BYTES_PER_ROW = 52   # child board written
+PIPELINE_BYTES_PER_BOARD = 901   # canonical unfused pipeline per evaluated board: child write 52
+                                 # + encode read 53 + fp16 feature write 396 + MLP read 396 + V write 4
 METRIC = "self-play env steps/sec (whole node) at 1-ply and 2-ply, 1/2/4/8 MI355X"
 
 
@@ -97,7 +99,8 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     w = load_weights()
     if world > 1:
         w = bdist.broadcast_weights(w)
-    eng = Engine(lanes=lanes, seed=args.seed, ply=ply, k_top=k_top, lane_base=rank * lanes)
+    eng = Engine(lanes=lanes, seed=args.seed, ply=ply, k_top=k_top, lane_base=rank * lanes,
+                 fused=not args.no_fused)
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
 
@@ -137,6 +140,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
         tm = eng.timing()
         d_tm = {k: s2[k] - s1[k] for k in s2}
         d_tm["elapsed_s"] = el_tm
+        d_tm["lanes"] = lanes
     eng.close()
     return el, d, tm, d_tm, gathered
 
@@ -148,9 +152,42 @@ def cpu_baseline(seconds, threads):
     return r
 
 
+def roofline_fused(d, tm):
+    """The fused 1-ply step kernel (one launch = all steps of a step() call):
+    the whole path's algorithmic bytes (54 B per movegen job +
+    901 B per evaluated board) and MLP FLOPs over its average launch."""
+    el = d["elapsed_s"]
+    n = max(1, tm["movegen_launches"])
+    launch = tm["movegen_ms"] / n
+    byts = (MOVEGEN_BYTES_PER_JOB * d["movegen_jobs"] + PIPELINE_BYTES_PER_BOARD * d["value_rows"]) / n
+    flop = MLP_FLOP_PER_ROW * d["value_rows"] / n
+    k = {"bound": "hbm", "achieved": byts / (launch * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "avg_launch_ms": launch, "launches": n, "steps_per_launch": d["env_steps"] / max(1, d["lanes"]) / n,
+         "share_of_wall": tm["movegen_ms"] * 1e-3 / el,
+         "basis": "54 B per movegen job + 901 B per evaluated board (SURVEY 8d canonical pipeline)"}
+    k["frac"] = k["achieved"] / k["peak"]
+    m = {"bound": "mfma", "achieved": flop / (launch * 1e-3) / 1e12, "peak": FP16_DENSE_PEAK_TFS,
+         "unit": "TFLOP/s", "avg_launch_ms": launch, "launches": n,
+         "basis": "50,944 FLOP per evaluated board (fp16x2 split: 2x that on the MFMA pipes)"}
+    m["frac"] = m["achieved"] / m["peak"]
+    r = {kk: k[kk] for kk in ("bound", "achieved", "peak", "unit", "frac")}
+    r["kernel"] = "bgx::fused_step_kernel (movegen + encode + MLP + select + env step, all steps of a launch)"
+    r["traffic"] = None
+    prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            with open(prof) as f:
+                r["traffic"] = json.load(f).get("1ply_fused", {}).get("fused", {}).get("hbm_bytes_per_launch")
+        except Exception:
+            r["traffic"] = None
+    return r, {"fused_step": k, "fused_step_mfma": m}
+
+
 def roofline_for(d, tm, leg):
     """Dominant kernel's algorithmic rate over its average launch (HIP events),
     from the timed pass `d` (stats deltas) / `tm` (event totals)."""
+    if tm["mlp_launches"] == 0 and tm["movegen_launches"] > 0:
+        return roofline_fused(d, tm)
     el = d["elapsed_s"]
     mg_ms, mlp_ms = tm["movegen_ms"], tm["mlp_ms"]
     out = {}
@@ -200,6 +237,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=7, help="mirrors src/main.py:86 (7 workers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="1-ply: one launch per phase and step instead of the fused persistent step kernel")
     ap.add_argument("--timing-steps", type=int, default=200,
                     help="length of the event-timed pass that feeds roofline (2-ply: min(this, 50))")
     args = ap.parse_args()
@@ -265,7 +304,9 @@ def main():
             "config": {"workload": f"{args.lanes} game lanes per GPU, {args.ply}-ply softmax select"
                                    + (" (configs[1])" if args.ply == 1 and args.lanes == 4096 else ""),
                        "lanes_per_gpu": args.lanes, "lanes_total": args.lanes * world, "ply": args.ply,
-                       "harvest_every": args.harvest_every, "parallelism": f"lanes sharded x{world}, "
+                       "harvest_every": args.harvest_every,
+                       "engine": "fused step kernel" if args.ply == 1 and not args.no_fused else "phased launches",
+                       "parallelism": f"lanes sharded x{world}, "
                        "RCCL episode gather" if world > 1 else "single GPU"},
             "decisions_per_s": sums["decisions"] / el,
             "episodes_per_s": sums["episodes"] / el,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 2
+#define BGX_ABI_VERSION 3
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -96,6 +96,9 @@ typedef struct bgx_config {
     int reply_per_lane;     /* average 2-ply reply rows reserved per lane */
     int greedy;             /* 1: argmax of the scores instead of sampling (play_versus_ai.py:188-195,
                                torch.argmax: first maximum); the sampling uniform is still drawn */
+    int fused;              /* 1-ply only, 1 (default): bgx_step runs as ONE persistent launch in which
+                               each 16-lane workgroup advances its lanes through all n_steps (movegen,
+                               MLP, select, step fused; same results as 0 = one launch per phase) */
 } bgx_config;
 
 void bgx_config_default(bgx_config* cfg);
@@ -150,7 +153,9 @@ int bgx_get_stats(bgx_engine* e, bgx_stats* out);  /* synchronizes */
 
 /* Kernel timing (HIP events on the engine stream, recorded per bgx_step while
  * enabled): total milliseconds and launch counts of the movegen and MLP
- * kernels since the last reset. */
+ * kernels since the last reset. A fused engine (bgx_config.fused, 1-ply)
+ * reports its one step kernel (all n_steps of a bgx_step) in the movegen slot
+ * and 0 MLP launches. */
 int bgx_set_timing(bgx_engine* e, int enabled);
 int bgx_get_timing(bgx_engine* e, double* ms_movegen, int* n_movegen, double* ms_mlp, int* n_mlp);
 

@@ -38,7 +38,7 @@ class Harvest:
 class Engine:
     def __init__(self, lanes=4096, seed=0, ply=1, k_top=4, device=None, lane_base=0, alpha=1.0,
                  beta=0.9, max_steps=300, max_legal=500, ring=640, ep_cap=0, cand_per_lane=256,
-                 reply_per_lane=0, greedy=False):
+                 reply_per_lane=0, greedy=False, fused=True):
         require_cuda()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         cfg = Config()
@@ -48,8 +48,10 @@ class Engine:
         cfg.max_steps, cfg.max_legal, cfg.ring, cfg.ep_cap = int(max_steps), int(max_legal), int(ring), int(ep_cap)
         cfg.cand_per_lane, cfg.reply_per_lane = int(cand_per_lane), int(reply_per_lane)
         cfg.greedy = 1 if greedy else 0
+        cfg.fused = 1 if fused else 0   # 1-ply: one persistent launch per step() call
         self.cfg = cfg
         self.lanes = int(lanes)
+        self.fused = bool(fused) and int(ply) == 1
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             check(lib().bgx_engine_create(self.device.index, ctypes.byref(cfg), ctypes.byref(h)),

@@ -146,6 +146,11 @@ struct bgx_engine {
     int ovf_cap = 0;
     uint32_t* ws = nullptr;
     int ws_waves = 0, ws_slots = 0;
+    // fused 1-ply step: per-lane candidate slots and values
+    bool fused = false;
+    uint32_t* fcand = nullptr;
+    float* fvbuf = nullptr;
+    int fcap = 0;
     // harvest
     uint32_t* out_records = nullptr;
     int out_cap = 0;
@@ -393,6 +398,7 @@ void bgx_config_default(bgx_config* c) {
     c->ep_cap = 0;   // 0 = derived from lanes
     c->cand_per_lane = 256;
     c->reply_per_lane = 0;   // 0 = derived from k_top
+    c->fused = 1;
 }
 
 int bgx_engine_destroy(bgx_engine* e) {
@@ -401,7 +407,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     hipDeviceSynchronize();
     void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
                   e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
-                  e->d_offs, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
+                  e->d_offs, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
                   e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
     for (void* p : ps) hipFree(p);
     for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
@@ -454,6 +460,16 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     e->ws_slots = 16384;
     ALLOC(e->ovf_list, e->ovf_cap);
     ALLOC(e->ws, (size_t)e->ws_waves * 5 * e->ws_slots);
+    e->fused = cfg->fused != 0 && cfg->ply == 1;
+    if (e->fused) {
+        e->fcap = cfg->max_legal;
+        if (e->fcap > 2048) {
+            bgx_engine_destroy(e);
+            return fail(BGX_E_ARG, "fused engine: max_legal=%d > 2048", cfg->max_legal);
+        }
+        ALLOC(e->fcand, (size_t)L * e->fcap * 8);
+        ALLOC(e->fvbuf, (size_t)L * (e->fcap + 1));
+    }
     if (cfg->ply == 2) {
         e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
         const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
@@ -649,6 +665,29 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
     return BGX_OK;
 }
 
+// fused 1-ply: one persistent launch for all n_steps (bgx_fused.hip)
+static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
+    bgx::FusedArgs f{};
+    f.e = e->d;
+    f.cand = e->fcand;
+    f.vbuf = e->fvbuf;
+    f.cap = e->fcap;
+    f.n_steps = n_steps;
+    f.wfrag = e->net->wfrag;
+    f.rowc = e->net->rowc;
+    f.b2 = e->net->b2;
+    f.feat_scale = e->net->feat_scale;
+    f.ws_global = e->ws;
+    f.ws_blocks = e->ws_waves;
+    f.ws_slots = e->ws_slots;
+    f.ws_words_per_block = (size_t)5 * e->ws_slots;
+    if (const char* v = getenv("BGX_MG_TEST_TIER")) f.force_tier = atoi(v);
+    if (timed(e, 0, s, true)) return BGX_E_HIP;
+    HIP_TRY(bgx_launch_fused(&f, s));
+    if (timed(e, 0, s, false)) return BGX_E_HIP;
+    return BGX_OK;
+}
+
 int bgx_step(bgx_engine* e, int n_steps, void* stream) {
     if (!e || n_steps < 0) return fail(BGX_E_ARG, "bgx_step: bad arguments");
     if (!e->net) return fail(BGX_E_STATE, "bgx_step: bgx_set_weights first");
@@ -662,6 +701,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
     // timed runs launch directly (events between the kernels); otherwise the
     // n_steps sequence is one graph launch (kernel arguments are fixed for the
     // engine's lifetime; bgx_set_weights drops the graph: temperature is an argument)
+    if (e->fused) return enqueue_fused(e, n_steps, s);
     if (e->timing || !e->use_graph) return enqueue_steps(e, n_steps, s);
     if (!e->gexec || e->g_steps != n_steps) {
         if (e->gexec) {

@@ -14,119 +14,9 @@
 //   1-ply V, score = alpha*S - beta*sum_rolls P(roll) * mean(top-5 replies),
 //   softmax(score/T) over the four; fewer than four moves fall back to 1-ply.
 // Dice / sampling randomness: Philox4x32-10 keyed by (seed, global lane id).
-#include "bgx_device.h"
-#include "bgx_kernels.h"
+#include "bgx_engine.h"
 
 namespace bgx {
-
-__constant__ float kRollProb[21] = {
-    1.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 1.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 2.f / 36,
-    1.f / 36, 2.f / 36, 2.f / 36, 2.f / 36, 1.f / 36, 2.f / 36, 2.f / 36, 1.f / 36, 2.f / 36, 1.f / 36};
-__constant__ double kRollProbD[21] = {
-    1. / 36, 2. / 36, 2. / 36, 2. / 36, 2. / 36, 2. / 36, 1. / 36, 2. / 36, 2. / 36, 2. / 36, 2. / 36,
-    1. / 36, 2. / 36, 2. / 36, 2. / 36, 1. / 36, 2. / 36, 2. / 36, 1. / 36, 2. / 36, 1. / 36};
-
-BGX_DEV uint64_t lane_key(uint64_t seed, uint32_t gid) {
-    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(gid + 1);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-struct LaneRng {
-    uint64_t key, ctr;
-    BGX_DEV u32x4 next() { return philox(key, 0x5EED0000ull, ctr++); }
-    BGX_DEV void roll(int& a, int& b) {
-        u32x4 r = next();
-        a = die_from(r.x);
-        b = die_from(r.y);
-    }
-};
-
-// packed initial board (immutable_board.py:27-70): P1 {0:2, 11:5, 16:3, 18:5}, P2 {23:2, 12:5, 7:3, 5:5}
-BGX_DEV void initial_packed(uint32_t* w) {
-    w[0] = 0x2u;                       // P1 point 0: 2
-    w[1] = 0x5u << 12;                 // P1 point 11: 5
-    w[2] = (0x3u << 0) | (0x5u << 8);  // P1 points 16: 3, 18: 5
-    w[3] = (0x5u << 20) | (0x3u << 28);// P2 points 5: 5, 7: 3
-    w[4] = 0x5u << 16;                 // P2 point 12: 5
-    w[5] = 0x2u << 28;                 // P2 point 23: 2
-    w[6] = 0;
-    w[7] = 0;
-}
-
-BGX_DEV void load_packed(const uint32_t* p, uint32_t* w) {
-    const uint4 x = ((const uint4*)p)[0], y = ((const uint4*)p)[1];
-    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-}
-BGX_DEV void store_packed(uint32_t* p, const uint32_t* w) {
-    ((uint4*)p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    ((uint4*)p)[1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
-BGX_DEV void set_flag(uint32_t* w, int p) { w[6] = (w[6] & 0xFFFFu) | ((uint32_t)p << 16); }
-
-// reset (backgammon_env.py:92-128); returns starter, leaves first dice in d0/d1
-BGX_DEV int new_game(LaneRng& rng, uint32_t* w, int& d0, int& d1) {
-    initial_packed(w);
-    int a, b;
-    do { rng.roll(a, b); } while (a == b);
-    const int starter = a < b ? 1 : 0;
-    do { rng.roll(a, b); } while (a == b);
-    d0 = a;
-    d1 = b;
-    set_flag(w, starter);
-    return starter;
-}
-
-BGX_DEV uint32_t pts_word(const uint32_t* w, int pl, int k) { return pl ? w[3 + k] : w[k]; }
-
-struct Outcome { float reward; int done, win_type, close, prime; };
-
-// env_helper.py:113-242 on a packed board after `pl` moved
-BGX_DEV Outcome judge(const uint32_t* w, int pl, uint32_t& flags) {
-    Outcome o = {0.0f, 0, 0, 0, 0};
-    const uint32_t s6 = w[6];
-    const int op = 1 - pl;
-    const uint32_t off_m = (s6 >> (8 + 4 * pl)) & 15u, off_o = (s6 >> (8 + 4 * op)) & 15u;
-    const uint32_t bar_o = (s6 >> (4 * op)) & 15u;
-    const uint32_t m0 = pts_word(w, pl, 0), m1 = pts_word(w, pl, 1), m2 = pts_word(w, pl, 2);
-    const uint32_t o0 = pts_word(w, op, 0), o1 = pts_word(w, op, 1), o2 = pts_word(w, op, 2);
-    const uint32_t occ_o = occ24(o0, o1, o2);
-    const uint32_t home = pl == 0 ? 0xFC0000u : 0x3Fu;
-    if (off_m >= 15u) {                                            // check_game_over
-        o.done = 1;
-        if (off_o == 0u && ((occ_o & home) || bar_o > 0u)) { o.reward = 2.5f; o.win_type = 3; }
-        else if (off_o == 0u) { o.reward = 2.0f; o.win_type = 2; }
-        else { o.reward = 1.0f; o.win_type = 1; }
-        return o;
-    }
-    const uint32_t g = ge2_24(m0, m1, m2);
-    float r = 0.0f;
-    const bool closed = bar_o > 0u && (g & home) == home;          // is_closed_out
-    if (closed && !(flags & (1u << pl))) {
-        r += 0.30f;
-        flags |= 1u << pl;
-        o.close = 1;
-    }
-    const uint32_t run5 = g & (g >> 1) & (g >> 2) & (g >> 3) & (g >> 4) & 0xFFFFFu;
-    bool prime = false;                                            // made_at_least_five_prime
-    if (run5) {
-        if (pl == 0) {
-            const int s = __ffs(run5) - 1;
-            prime = (occ_o >> (s + 5)) != 0u;
-        } else {
-            const int s = 31 - __clz(run5);
-            prime = (occ_o & ((1u << s) - 1u)) != 0u;
-        }
-    }
-    if (prime && !(flags & (4u << pl))) {
-        r += 0.20f;
-        flags |= 4u << pl;
-        o.prime = 1;
-    }
-    o.reward = r;
-    return o;
-}
 
 __global__ __launch_bounds__(256) void engine_reset_kernel(EngineDev e) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -148,90 +38,6 @@ __global__ __launch_bounds__(256) void engine_reset_kernel(EngineDev e) {
     e.harv[i] = 0;
 }
 
-// One game lane's env step after its action is chosen (BackgammonEnv.step,
-// backgammon_env.py:130-221, + the worker's Experience, worker.py:101-162):
-// apply, judge, record, and on game end append the episode header and reset.
-// action < 0 (or no legal move): pass.
-BGX_DEV void step_lane(const EngineDev& e, int i, int action) {
-    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), e.rng[i]};
-    int p = e.player[i];
-    int steps = e.step[i];
-    uint32_t flags = e.flags[i];
-    uint32_t w[8];
-    load_packed(e.rows + (size_t)i * 8, w);
-    const int n_full = e.cand_cnt[i];
-    const int n = n_full < e.max_legal ? n_full : e.max_legal;
-    const int base = e.L + e.cand_off[i];
-    int d0 = e.dice[2 * i], d1 = e.dice[2 * i + 1];
-    bool done = false;
-    int win_type = 0, winner = -1;
-    if (n == 0 || action < 0) {
-        // pass (backgammon_env.py:139-151): no experience is recorded (worker.py:106-113)
-        p ^= 1;
-        rng.roll(d0, d1);
-    } else {
-        flags |= 16u << p;
-        rng.ctr++;   // the select kernel's sampling uniform
-        const int a = action;
-        uint32_t nb[8];
-        load_packed(e.rows + (size_t)(base + a) * 8, nb);
-        const int mover = p;
-        const Outcome o = judge(nb, mover, flags);
-        done = o.done;
-        if (done) { win_type = o.win_type; winner = mover; }
-        else { p ^= 1; rng.roll(d0, d1); }
-        // experience record (worker.py:149-156; Experience, episode.py:5-46)
-        const uint32_t rec = e.rec_count[i];
-        if (rec - e.harv[i] >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
-        uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
-        uint32_t before[8];
-        for (int k = 0; k < 8; ++k) before[k] = w[k];
-        set_flag(before, mover);
-        set_flag(nb, done ? mover : p);
-        store_packed(R, before);
-        store_packed(R + 8, nb);
-        const float vs = e.V[i], va = e.V[base + a];
-        const int dd0 = e.dice[2 * i], dd1 = e.dice[2 * i + 1];
-        uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
-                                 (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
-        uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
-                                     ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
-                                     ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
-                                 e.epi[i], (uint32_t)steps, (uint32_t)(e.lane_base + i));
-        ((uint4*)(R + 16))[0] = tail0;
-        ((uint4*)(R + 16))[1] = tail1;
-        e.rec_count[i] = rec + 1;
-        for (int k = 0; k < 8; ++k) w[k] = nb[k];
-    }
-    ++steps;
-    set_flag(w, p);
-    if (done || steps >= e.max_steps) {
-        const uint32_t slot = atomicAdd(e.ep_count, 1u);
-        if ((int)slot < e.ep_cap) {
-            uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
-            const uint32_t first = e.ep_first[i], nrec = e.rec_count[i] - first;
-            ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), e.epi[i], first, nrec);
-            ((uint4*)h)[1] = make_uint4((uint32_t)steps,
-                                        (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
-                                            (flags << 16),
-                                        0u, 0u);
-        } else {
-            atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
-        }
-        p = new_game(rng, w, d0, d1);
-        steps = 0;
-        flags = 0;
-        e.epi[i] = e.epi[i] + 1;
-        e.ep_first[i] = e.rec_count[i];
-    }
-    store_packed(e.rows + (size_t)i * 8, w);
-    e.player[i] = (uint8_t)p;
-    e.dice[2 * i] = (uint8_t)d0;
-    e.dice[2 * i + 1] = (uint8_t)d1;
-    e.step[i] = steps;
-    e.flags[i] = flags;
-    e.rng[i] = rng.ctr;
-}
 
 // Action selection, one wavefront per game lane:
 //   1-ply: softmax(V[1:] / T) + Categorical sample (worker.py:137-143);
@@ -296,50 +102,7 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
         x[k] = v;
     }
     wave_sync();
-    float mx = -INFINITY;
-    for (int k = l; k < m; k += 64) mx = fmaxf(mx, x[k]);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-    float sum = 0.0f;
-    for (int k = l; k < m; k += 64) sum += __expf(x[k] - mx);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 64);
-    int pick = m - 1;
-    if (e.greedy) {
-        // argmax, first maximum (torch.argmax; the temperature does not change it)
-        float bv = -INFINITY;
-        int bk = 0x7FFFFFFF;
-        for (int k = l; k < m; k += 64)
-            if (x[k] > bv) { bv = x[k]; bk = k; }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const float ov = __shfl_xor(bv, off, 64);
-            const int ok = __shfl_xor(bk, off, 64);
-            if (ov > bv || (ov == bv && ok < bk)) { bv = ov; bk = ok; }
-        }
-        if (l == 0) step_lane(e, i, k4 ? e.sel[4 * i + bk] - base : bk);
-        return;
-    }
-    const uint64_t key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
-    const float u = unit_from(philox(key, 0x5EED0000ull, e.rng[i]).x);
-    const float t = u * sum;
-    float carry = 0.0f;
-    for (int b = 0; b < m; b += 64) {
-        const int k = b + l;
-        float p = k < m ? __expf(x[k] - mx) : 0.0f;
-        // inclusive scan of p over the wave
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const float q = __shfl_up(p, off, 64);
-            if (l >= off) p += q;
-        }
-        const uint64_t hit = ballot(k < m && t < carry + p);
-        if (hit) {
-            pick = b + __ffsll((unsigned long long)hit) - 1;
-            break;
-        }
-        carry += __shfl(p, 63, 64);
-    }
+    const int pick = pick_action(x, m, e.greedy != 0, lane_uniform(e, i));
     if (l == 0) step_lane(e, i, k4 ? e.sel[4 * i + pick] - base : pick);
 }
 

@@ -112,11 +112,31 @@ struct EngineDev {
     unsigned* err_flags;
 };
 
+// Fused 1-ply lane step (bgx_fused.hip): one persistent launch runs n_steps
+// env steps of every lane; 16 lanes per workgroup advance together.
+struct FusedArgs {
+    EngineDev e;
+    uint32_t* cand;              // [L][cap][8] packed candidate rows, lane-major
+    float* vbuf;                 // [L][cap + 1] V(s), then V(candidate k) at 1 + k
+    int cap;                     // candidate slots per lane (= max_legal: later moves are never read)
+    int n_steps;
+    const uint4* wfrag;          // split-fp16 W fragments (MlpArgs::wfrag)
+    const float* rowc;           // [128] w2
+    float b2;
+    float feat_scale;
+    uint32_t* ws_global;         // tier-3 movegen workspace, one slice per workgroup
+    int ws_blocks;               // slices (>= gridDim.x)
+    int ws_slots;
+    size_t ws_words_per_block;
+    int force_tier;              // test hook (BGX_MG_TEST_TIER)
+};
+
 }  // namespace bgx
 
 extern "C" {
 hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream_t stream);
 hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t stream);
+hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t stream);
 hipError_t bgx_launch_encode(const uint8_t* boards, const uint8_t* player, int n, float* out,
                              int layout, hipStream_t stream);
 hipError_t bgx_launch_value_f32(const float* x, int n, const float* W1, const float* b1,

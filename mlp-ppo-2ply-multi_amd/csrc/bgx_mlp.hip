@@ -26,65 +26,11 @@
 // registers from the 32-byte packed board (no feature tensor in HBM).
 // W fragments (2 terms x 4 m-tiles x 13 k-steps x 64 lanes x 16 B = 104 KB)
 // stay resident in LDS; one persistent 512-thread workgroup per CU.
-#include "bgx_device.h"
-#include "bgx_kernels.h"
+#include "bgx_mlp.h"
 
 #include <cstdlib>
 
 namespace bgx {
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int KSTEPS = 13;   // 208 = 13 x 16 >= 198
-constexpr int NFRAG = 2 * 4 * KSTEPS * 64;
-
-BGX_DEV _Float16 hf(float v) { return (_Float16)v; }
-
-// B fragment (8 features of one board) for k-step s (0..12), lane half h
-BGX_DEV half8 feat_frag(const uint4 x, const uint4 y, int s, int h, const uint4* lut, float sc) {
-    if (s < 12) {
-        // point slots q0 = 4s + 2h and q0 + 1 = byte (2(s&1) + h) of word s >> 1
-        const int wi = s >> 1;
-        uint32_t word = x.x;
-        word = wi == 1 ? x.y : word;
-        word = wi == 2 ? x.z : word;
-        word = wi == 3 ? x.w : word;
-        word = wi == 4 ? y.x : word;
-        word = wi == 5 ? y.y : word;
-        const uint32_t byte = (word >> (8 * (2 * (s & 1) + h))) & 0xFFu;
-        const uint4 f = lut[byte];
-        return *(const half8*)&f;
-    }
-    half8 f;
-    const uint32_t s6 = y.z;
-    const float on = h == 0 ? sc : 0.0f;   // features carry the 2^-e scale
-    const uint32_t flag = (s6 >> 16) & 1u;
-    f[0] = hf(on * (float)(s6 & 15u) * 0.5f);          // bar1 / 2
-    f[1] = hf(on * (float)((s6 >> 8) & 15u));          // off1 (W col / 15)
-    f[2] = hf(on * (float)((s6 >> 4) & 15u) * 0.5f);   // bar2 / 2
-    f[3] = hf(on * (float)((s6 >> 12) & 15u));         // off2 (W col / 15)
-    f[4] = hf(on * (flag == 0u ? 1.0f : 0.0f));        // PLAYER1 to play
-    f[5] = hf(on * (flag == 1u ? 1.0f : 0.0f));        // PLAYER2 to play
-    f[6] = hf(on);                                     // bias feature (W col 198 = b1)
-    f[7] = (_Float16)0.0f;
-    return f;
-}
-
-// LUT entry for byte b: features [n>=1, n>=2, n>=3, max(n-3,0)/2] of n = b & 15, then of b >> 4,
-// times the 2^-e scale
-BGX_DEV uint4 lut_entry(uint32_t b, float sc) {
-    half8 f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int n = (int)((b >> (4 * t)) & 15u);
-        f[4 * t + 0] = (_Float16)(n >= 1 ? sc : 0.0f);
-        f[4 * t + 1] = (_Float16)(n >= 2 ? sc : 0.0f);
-        f[4 * t + 2] = (_Float16)(n >= 3 ? sc : 0.0f);
-        f[4 * t + 3] = (_Float16)(n > 3 ? (float)(n - 3) * 0.5f * sc : 0.0f);
-    }
-    return *(const uint4*)&f;
-}
 
 BGX_DEV void load_rows(const MlpArgs& a, int n, int t, int NTq, int col, uint4& x, uint4& y) {
     const int row = t * 32 + col;

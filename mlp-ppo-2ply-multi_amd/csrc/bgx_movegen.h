@@ -1,0 +1,1025 @@
+// bgx_movegen.h — K2 device code (move generation + afterstate expansion), shared by
+// the movegen kernels (bgx_movegen.hip) and the fused 1-ply lane kernel (bgx_fused.hip).
+// Algorithm notes: see the header comment of bgx_movegen.hip.
+#pragma once
+#include "bgx_device.h"
+#include "bgx_kernels.h"
+
+#include <cstdlib>
+
+namespace bgx {
+
+constexpr unsigned long long EMPTY64 = ~0ull;
+constexpr uint32_t KEY_EMPTY4 = 0xFFFFFu;   // four empty 5-bit fields
+constexpr uint32_t KEYMASK = 0xFFFFFu;
+constexpr uint32_t FLAG1 = 0x80000000u;      // "parent had exactly one move"
+// LDS slices: tier 1 runs every job in SLICE_T1 bytes (512-slot table + two
+// 512-entry frontiers = 8 KB, 20 waves per CU); a job whose level outgrows it
+// is re-run by tier 2 in a 32 KB slice (2048 slots), and what still overflows
+// by the global-memory kernel. Results are identical in every tier.
+// slice = table [S] u64 | fa [S - 32] u32 | fb [S - 32] u32 | map [64] u32
+template <int S> struct Slice { static constexpr int F = S - 32, bytes = S * 8 + 2 * F * 4 + 64 * 4; };
+constexpr int S_T1 = 512;
+constexpr int S_T2 = 2048;
+
+struct Mem {
+    unsigned long long* tab;   // [S]
+    uint32_t* fa;              // [F]
+    uint32_t* fb;              // [F]
+    uint32_t* map;             // [64] parent start marks for one child chunk (kept zero between uses)
+    int S, F;
+    int exp = 0;               // development experiments (MovegenArgs::exp_mode)
+};
+
+// LDS (wavefront scope) or global (agent scope) accessors
+template <bool G> BGX_DEV uint32_t ld32(const uint32_t* p) {
+    if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV void st32(uint32_t* p, uint32_t v) {
+    if constexpr (G) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV unsigned long long ld64(const unsigned long long* p) {
+    if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV void st64(unsigned long long* p, unsigned long long v) {
+    if constexpr (G) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV unsigned long long cas64(unsigned long long* p, unsigned long long v) {
+    unsigned long long cmp = EMPTY64;
+    if constexpr (G)
+        __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return cmp;
+}
+template <bool G> BGX_DEV void min64(unsigned long long* p, unsigned long long v) {
+    if constexpr (G) __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <bool G> BGX_DEV void sync() {
+    if constexpr (G) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    } else {
+        wave_sync();
+    }
+}
+template <bool G> BGX_DEV void clear_tab(const Mem& M) {
+    for (int i = lane_id(); i < M.S; i += 64) st64<G>(M.tab + i, EMPTY64);
+    sync<G>();
+}
+
+BGX_DEV uint32_t hash32(uint32_t k) {
+    k ^= k >> 15;
+    k *= 0x2C1B3C6Du;
+    k ^= k >> 12;
+    k *= 0x297A2D39u;
+    return k ^ (k >> 15);
+}
+
+// Insert (key, ord) for active lanes; returns the slot holding each lane's key.
+// `fresh` = this lane's CAS created the slot (a key new to the table).
+template <bool G>
+BGX_DEV uint32_t dedup_insert(const Mem& M, bool active, uint32_t key, uint32_t ord, bool& fresh) {
+    const uint32_t mask = (uint32_t)M.S - 1u;
+    uint32_t slot = hash32(key) & mask;
+    const unsigned long long v = ((unsigned long long)key << 32) | ord;
+    bool pending = active;
+    fresh = false;
+    while (ballot(pending)) {
+        if (pending) {
+            const unsigned long long old = cas64<G>(M.tab + slot, v);
+            if (old == EMPTY64) {
+                pending = false;
+                fresh = true;
+            } else if ((uint32_t)(old >> 32) == key) {
+                if ((uint32_t)old > ord) min64<G>(M.tab + slot, v);
+                pending = false;
+            } else {
+                slot = (slot + 1u) & mask;
+            }
+        }
+    }
+    return slot;
+}
+
+// ------------------------------------------------------------------ keys
+// doubles: sorted multiset of relative step sources (0 = BAR, then travel order)
+BGX_DEV uint32_t rel_of(int s, int player) {
+    if (s == 24) return 0u;
+    return player == 0 ? (uint32_t)(s + 1) : (uint32_t)(24 - s);
+}
+BGX_DEV int abs_of(uint32_t rel, int player) {
+    if (rel == 0u) return 24;
+    return player == 0 ? (int)rel - 1 : 24 - (int)rel;
+}
+BGX_DEV uint32_t key_insert(uint32_t key, uint32_t rel) {
+    uint32_t out = 0;
+    int o = 0;
+    bool placed = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t f = (key >> (5 * i)) & 31u;
+        if (!placed && rel <= f) { out |= rel << (5 * o); ++o; placed = true; }
+        if (o < 4) { out |= f << (5 * o); ++o; }
+    }
+    return out;
+}
+BGX_DEV Node rebuild(const Root& R, uint32_t key, int d) {
+    Node n = root_node(R);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t f = (key >> (5 * i)) & 31u;
+        if (f != 31u) n = apply_move(R, n, abs_of(f, R.player), d);
+    }
+    return n;
+}
+
+// ---- doubles without a table (first-reach paths only) ----------------------
+// Outside bear-off a node's move list is its movable sources in ascending
+// position (bar entry alone while on the bar), so the first-reach path of a
+// board (the lexicographically smallest index sequence, which the reference's
+// DFS records) takes, at every step, the lowest source movable there. A path
+// is first-reach iff no later step uses a source that was movable, and lower,
+// at an earlier step. Keeping only such paths gives every board once, already
+// in first-reach order: no hash table, no dedup, no duplicate children.
+// Valid when no node of the tree can be in bear-off (>= 5 mover checkers
+// outside home, bar included); other jobs take the table path.
+constexpr uint32_t PATHF = 0x40000000u;        // frontier / record entry is a path
+constexpr uint32_t PATH_EMPTY = KEY_EMPTY4;   // four empty 5-bit fields
+
+BGX_DEV bool doubles_by_path(const Root& R) {
+    const uint32_t home = R.player == 0 ? nibsum(R.m2 >> 8) : nibsum(R.m0 & 0xFFFFFFu);
+    return 15u - R.off - home >= 5u;   // outside home (points and bar)
+}
+// node after the path's steps (abs sources, in order) and the sources the
+// path rules out: movable at an earlier step and below that step's source
+BGX_DEV Node path_node(const Root& R, uint32_t path, int d, uint32_t okd, uint32_t& bad) {
+    Node n = root_node(R);
+    bad = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t f = (path >> (5 * i)) & 31u;
+        if (f != 31u) {
+            if (f < 24u) bad |= occ24(n.m0, n.m1, n.m2) & okd & ((1u << f) - 1u);
+            n = apply_move(R, n, (int)f, d);
+        }
+    }
+    return n;
+}
+BGX_DEV Node path_board(const Root& R, uint32_t path, int d) {
+    Node n = root_node(R);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t f = (path >> (5 * i)) & 31u;
+        if (f != 31u) n = apply_move(R, n, (int)f, d);
+    }
+    return n;
+}
+
+// non-doubles: positions 0..23 points, 24 = BAR (source), 25 = OFF (dest), 31 = none
+BGX_DEV int dest_of(const Root& R, int s, int d) {
+    const int t = s == 24 ? (R.player == 0 ? d - 1 : 24 - d) : (R.player == 0 ? s + d : s - d);
+    return (t < 0 || t > 23) ? 25 : t;
+}
+BGX_DEV uint32_t sort2(uint32_t a, uint32_t b) { return a <= b ? (a | (b << 5)) : (b | (a << 5)); }
+// canonical key of the board after steps (s1->t1, hit h1) and (s2->t2, hit h2); s2 = 31: single
+BGX_DEV uint32_t nd_key(uint32_t s1, uint32_t t1, bool h1, uint32_t s2, uint32_t t2, bool h2) {
+    uint32_t r0 = s1, r1 = s2, a0 = t1, a1 = t2;
+    if (s2 != 31u) {
+        if (t1 == s2) { r1 = 31u; a0 = 31u; }        // chained checker: s1 -> t1 -> t2
+        else if (t2 == s1) { r0 = 31u; a1 = 31u; }   // s2 -> s1 -> t1
+    }
+    const uint32_t hh0 = h1 ? t1 : 31u, hh1 = h2 ? t2 : 31u;
+    return sort2(r0, r1) | (sort2(a0, a1) << 10) | (sort2(hh0, hh1) << 20);
+}
+
+// Non-doubles without a table. With nothing on the bar and >= 3 mover
+// checkers outside home no node of the two-step tree is in bear-off, and the
+// 2-move plays enumerated in (pass, i, j) order (pass 0: high die first) fall
+// into two kinds:
+//  - two checkers (no step lands on the other's source): the pass-0 play
+//    (a with H, b with L) is the only pass-0 producer of its board and its
+//    pass-1 twin (b with L, a with H) is always legal: keep pass 0 only;
+//  - one checker x moving H + L: producers A = pass-0 chain x -> x+H -> .,
+//    B = pass-0 reverse (x+L with H, then x with L; x+L mover-occupied),
+//    C = pass-1 chain x -> x+L -> ., D = pass-1 reverse (x+H with L, then x
+//    with H). A chain that hits at its intermediate point makes a board no
+//    other play makes; the others make the same board and the first legal one
+//    in enumeration order (ascending first source within a pass) is kept.
+// This reproduces first-occurrence dedup (handle_non_doubles,
+// generate_all_moves.py:28-68) exactly on those positions; others use the table.
+constexpr uint32_t ND_DROP = 0xFFFFFFFFu;
+BGX_DEV bool nd_by_rule(const Root& R) {
+    const uint32_t home = R.player == 0 ? nibsum(R.m2 >> 8) : nibsum(R.m0 & 0xFFFFFFu);
+    return R.bar == 0u && 15u - R.off - home >= 3u;
+}
+BGX_DEV bool nd_first(const Root& R, uint32_t occ0, int pass, int s1, int t1, int s2, int t2, int H, int L) {
+    const bool chain = s2 == t1;
+    if (!chain && t2 != s1) return pass == 0;
+    if (chain && ((R.blot >> t1) & 1u)) return true;
+    const int x = chain ? s1 : s2;
+    const int iH = R.player == 0 ? x + H : x - H, iL = R.player == 0 ? x + L : x - L;
+    const uint32_t bad = R.block | R.blot;
+    const bool A = !((bad >> iH) & 1u), B = (occ0 >> iL) & 1u;
+    const bool C = !((bad >> iL) & 1u), D = (occ0 >> iH) & 1u;
+    // rank in enumeration order: player 0 (sources ascend with travel) A B C D,
+    // player 1 B A D C
+    const int me = pass == 0 ? (chain ? 0 : 1) : (chain ? 2 : 3);
+    const bool p0 = R.player == 0;
+    switch (me) {
+        case 0: return p0 ? true : !B;
+        case 1: return p0 ? !A : true;
+        case 2: return !A && !B && (p0 ? true : !D);
+        default: return !A && !B && (p0 ? !C : true);
+    }
+}
+BGX_DEV void nib_add(Node& n, int p, int delta) {
+    const uint32_t v = 1u << ((p & 7) * 4);
+    const int w = p >> 3;
+    if (delta > 0) {
+        n.m0 += w == 0 ? v : 0u; n.m1 += w == 1 ? v : 0u; n.m2 += w == 2 ? v : 0u;
+    } else {
+        n.m0 -= w == 0 ? v : 0u; n.m1 -= w == 1 ? v : 0u; n.m2 -= w == 2 ? v : 0u;
+    }
+}
+BGX_DEV Node nd_board(const Root& R, uint32_t key) {
+    Node n = root_node(R);
+    // additions first, so a removal never borrows from a neighbouring nibble
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t a = (key >> (10 + 5 * i)) & 31u, h = (key >> (20 + 5 * i)) & 31u;
+        if (a == 25u) n.x += 16u;
+        else if (a < 24u) nib_add(n, (int)a, +1);
+        if (h < 24u) n.x |= 1u << (8 + h);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t r = (key >> (5 * i)) & 31u;
+        if (r == 24u) n.x -= 1u;
+        else if (r < 24u) nib_add(n, (int)r, -1);
+    }
+    return n;
+}
+
+// ------------------------------------------------------------------ job I/O
+struct JobIn { Root R; int d0, d1; bool skip; };
+
+BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
+    JobIn in;
+    uint32_t w0, w1, w2, w3, w4, w5, w6;
+    int player = 0;
+    in.skip = false;
+    if (a.in_mode == IN_U8) {
+        const uint32_t* b = (const uint32_t*)(a.in_u8 + (size_t)j * 52);
+        w0 = pack4(b[0]) | (pack4(b[1]) << 16);
+        w1 = pack4(b[2]) | (pack4(b[3]) << 16);
+        w2 = pack4(b[4]) | (pack4(b[5]) << 16);
+        w3 = pack4(b[6]) | (pack4(b[7]) << 16);
+        w4 = pack4(b[8]) | (pack4(b[9]) << 16);
+        w5 = pack4(b[10]) | (pack4(b[11]) << 16);
+        const uint32_t t = b[12];
+        w6 = (t & 15u) | (((t >> 8) & 15u) << 4) | (((t >> 16) & 15u) << 8) | (((t >> 24) & 15u) << 12);
+        player = a.in_player[j];
+        in.d0 = a.in_dice[2 * j];
+        in.d1 = a.in_dice[2 * j + 1];
+    } else {
+        int src = j;
+        if (a.in_mode == IN_TWOPLY) {
+            const int row = j / 21;
+            src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
+            if (src < 0) {
+                in.skip = true;
+                src = 0;
+            }
+        }
+        const uint4* p = (const uint4*)(a.in_packed + (size_t)src * 8);
+        const uint4 x = p[0], y = p[1];
+        w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w; w4 = y.x; w5 = y.y; w6 = y.z;
+        if (a.in_mode == IN_TWOPLY) {
+            // two_ply.py:93-150: the opponent of the candidate's mover replies to every roll
+            player = 1 - (int)((w6 >> 16) & 1u);
+            int a0 = 1, r = j - 21 * (j / 21);   // DICE_ROLLS order (two_ply.py:10-32)
+            while (r >= 7 - a0) { r -= 7 - a0; ++a0; }
+            in.d0 = a0;
+            in.d1 = a0 + r;
+        } else {
+            player = a.in_player[j];
+            in.d0 = a.in_dice[2 * j];
+            in.d1 = a.in_dice[2 * j + 1];
+        }
+    }
+    // the job is wave-uniform: pin its words in SGPRs so the root analysis
+    // below (and node_moves on the root) runs on the scalar unit, not VALU
+    w0 = uniformu(w0); w1 = uniformu(w1); w2 = uniformu(w2); w3 = uniformu(w3);
+    w4 = uniformu(w4); w5 = uniformu(w5); w6 = uniformu(w6);
+    player = uniform(player);
+    in.d0 = uniform(in.d0);
+    in.d1 = uniform(in.d1);
+    const bool p2 = player != 0;
+    Root& R = in.R;
+    R.m0 = p2 ? w3 : w0; R.m1 = p2 ? w4 : w1; R.m2 = p2 ? w5 : w2;
+    R.o0 = p2 ? w0 : w3; R.o1 = p2 ? w1 : w4; R.o2 = p2 ? w2 : w5;
+    const uint32_t b0 = w6 & 15u, b1 = (w6 >> 4) & 15u, f0 = (w6 >> 8) & 15u, f1 = (w6 >> 12) & 15u;
+    R.bar = p2 ? b1 : b0; R.obar = p2 ? b0 : b1;
+    R.off = p2 ? f1 : f0; R.ooff = p2 ? f0 : f1;
+    R.block = ge2_24(R.o0, R.o1, R.o2);
+    R.blot = occ24(R.o0, R.o1, R.o2) & ~R.block;
+    R.player = player;
+    return in;
+}
+
+// write record k of job j (lane-local)
+BGX_DEV void emit_one(const MovegenArgs& a, int j, const Root& R, const Node& n, int k, int base) {
+    uint32_t w[8];
+    node_to_packed(R, n, (uint32_t)R.player, w);
+    if (a.out_mode == OUT_U8) {
+        if (k >= a.cap) return;
+        uint32_t o[13];
+        packed_to_u8(w, o);
+        uint32_t* dst = (uint32_t*)(a.out_u8 + ((size_t)j * a.cap + k) * 52);
+#pragma unroll
+        for (int i = 0; i < 13; ++i) dst[i] = o[i];
+        return;
+    }
+    size_t row;
+    if (a.out_mode == OUT_PACKED_SLOT) {
+        if (k >= a.cap) return;
+        row = (size_t)j * a.cap + k;
+    } else {
+        row = (size_t)base + k;
+    }
+    uint4* dst = (uint4*)(a.out_packed + row * 8);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+BGX_DEV int job_count(const MovegenArgs& a) {
+    int n = a.n_jobs;
+    if (a.n_jobs_dev) n += (int)(*a.n_jobs_dev) * a.jobs_per_dev_unit;
+    if (a.n_jobs_max > 0 && n > a.n_jobs_max) n = a.n_jobs_max;
+    return n;
+}
+
+// Per-wave output reservation for OUT_PACKED_FLAT: one global atomic per
+// `flat_chunk` rows instead of one per job (a single counter hit by every job
+// of a 2-ply launch serialises at the memory side).
+struct FlatCursor { int base = 0, left = 0; };
+
+// reserve output space once the job's record count is known; returns base (-1: overflow)
+BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
+    int base = 0;
+    if (a.out_mode == OUT_PACKED_FLAT) {
+        if (n <= fc.left) {
+            base = fc.base;
+            fc.base += n;
+            fc.left -= n;
+        } else {
+            // chunk = min(flat_chunk, 32 rows per job this wave still has), at least n
+            const int left_jobs = (job_count(a) - j + (int)gridDim.x - 1) / (int)gridDim.x;
+            int want = 32 * left_jobs;
+            if (want > a.flat_chunk) want = a.flat_chunk;
+            const int grab = n > want ? n : want;
+            if (lane_id() == 0) base = (int)atomicAdd(a.flat_count, (unsigned)grab);
+            base = uniform(base);
+            if (base + grab > a.flat_cap) {
+                if (lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
+                fc.left = 0;
+                base = -1;
+            } else {
+                fc.base = base + n;
+                fc.left = grab - n;
+            }
+        }
+        if (lane_id() == 0) {
+            a.job_off[j] = base < 0 ? 0 : base;
+            a.job_cnt[j] = base < 0 ? 0 : n;
+        }
+    } else if (lane_id() == 0) {
+        a.out_count[j] = n;
+    }
+    return base;
+}
+
+// ------------------------------------------------------------------ expansion
+// j-th set bit (0-based) of a 24-bit mask, j < popcount(m): branch-free narrowing
+BGX_DEV int select_bit_fast(uint32_t m, int j) {
+    int base = 0;
+    int c = __popc(m & 0xFFFu);
+    if (j >= c) { j -= c; m >>= 12; base += 12; }
+    c = __popc(m & 0x3Fu);
+    if (j >= c) { j -= c; m >>= 6; base += 6; }
+    c = __popc(m & 0x7u);
+    if (j >= c) { j -= c; m >>= 3; base += 3; }
+    m = j >= 1 ? (m & (m - 1u)) : m;
+    m = j >= 2 ? (m & (m - 1u)) : m;
+    return base + __ffs(m) - 1;
+}
+
+// would appending T entries at n overflow a list of F?
+BGX_DEV bool n_out_check(int n, int T, int F) { return n + T > F; }
+
+// Parent lane of child r = b + lane in a flat enumeration: the last lane q
+// with c > 0 and excl <= r. Parents starting inside [b, b + 64) mark
+// map[excl - b] = q + 1; a max-scan over the marks fills the gaps; before the
+// first mark it is q0. `map` (64 words) is zero on entry and on return.
+template <bool G>
+BGX_DEV int flat_parent(uint32_t* map, int excl, int c, int b) {
+    const int l = lane_id();
+    const int st = excl - b;
+    if (c > 0 && st >= 0 && st < 64) st32<G>(map + st, (uint32_t)(l + 1));
+    const uint64_t cov = ballot(c > 0 && excl <= b);
+    const int q0 = cov ? 63 - __clzll((long long)cov) : 0;
+    sync<G>();
+    const int mk = wave_incl_max((int)ld32<G>(map + l));
+    st32<G>(map + l, 0u);
+    return mk ? mk - 1 : q0;
+}
+
+// Expand one chunk of parents (one per lane, c = its move count, c = 0 for
+// none). Children are enumerated FLAT in (parent, move) = ordinal order, one
+// per lane: the parent is the largest lane p with exclusive-prefix <= r (six
+// shuffle steps), its move list comes over by shuffles, kfn(p, s) gives the
+// child's key. Each 64-child chunk is deduplicated in one round; survivors
+// (first occurrences) are appended to `out` in order with payload key | tag.
+// Returns false when the table or the list would overflow (fallback path).
+template <bool G, typename KeyFn>
+BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, uint32_t ord_base, KeyFn kfn,
+                         uint32_t* out, int& n_out, int& inserted, uint32_t& total) {
+    const int l = lane_id();
+    const int incl = wave_incl_scan(c);
+    const int excl = incl - c;
+    const int T = lane63(incl);
+    total = (uint32_t)T;
+    for (int b = 0; b < T; b += 64) {
+        const int r = b + l;
+        const bool act = r < T;
+        const int p = flat_parent<G>(M.map, excl, c, b);
+        const int j = r - __shfl(excl, p, 64);
+        const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+        const int nsrc = __shfl(pm.nsrc, p, 64);
+        const int e0 = __shfl(pm.e0, p, 64), e1 = __shfl(pm.e1, p, 64);
+        const uint32_t tag = (uint32_t)__shfl((int)tagbit, p, 64);
+        const int s = j < nsrc ? select_bit_fast(src, j) : (j == nsrc ? e0 : e1);
+        const uint32_t key = kfn(p, s);
+        const uint32_t ord = ord_base + (uint32_t)r;
+        bool fresh;
+        uint32_t slot = 0;
+        if (M.exp & 2) fresh = act;
+        else slot = dedup_insert<G>(M, act, key, ord, fresh);
+        inserted += __popcll(ballot(fresh));
+        if (inserted > M.S - (M.S >> 2) || n_out + 64 > M.F) return false;
+        sync<G>();
+        const bool sv = act && ((M.exp & 2) ? true : (uint32_t)ld64<G>(M.tab + slot) == ord);
+        const uint64_t bm = ballot(sv);
+        if (sv) st32<G>(out + n_out + mask_prefix(bm), key | tag);
+        n_out += __popcll(bm);
+    }
+    sync<G>();
+    return true;
+}
+
+// expand_flat without a table: kfn returns ND_DROP for children that an
+// earlier child already produced (nd_first); the rest are appended in order
+template <bool G, typename KeyFn>
+BGX_DEV bool expand_keep(const Mem& M, const Moves& pm, int c, KeyFn kfn, uint32_t* out, int& n_out) {
+    const int l = lane_id();
+    const int incl = wave_incl_scan(c);
+    const int excl = incl - c;
+    const int T = lane63(incl);
+    for (int b = 0; b < T; b += 64) {
+        const int r = b + l;
+        const int p = flat_parent<G>(M.map, excl, c, b);
+        const int j = r - __shfl(excl, p, 64);
+        const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+        // kfn shuffles from the parent lane: every lane runs it (a lane
+        // masked off by a branch returns nothing to ds_bpermute)
+        const uint32_t key = kfn(p, select_bit_fast(src, j));
+        const bool sv = r < T && key != ND_DROP;
+        const uint64_t bm = ballot(sv);
+        if (n_out + 64 > M.F) return false;
+        if (sv) st32<G>(out + n_out + mask_prefix(bm), key);
+        n_out += __popcll(bm);
+    }
+    sync<G>();
+    return true;
+}
+
+// ------------------------------------------------------------------ the job
+// returns the record count, or -1 when the slice overflowed (fallback)
+// heavy_t: a doubles level with more children than this returns -2 (the
+// small-launch kernel then expands the job with the whole block)
+template <bool G>
+BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int heavy_t) {
+    const Root& R = in.R;
+    const int l = lane_id();
+    const Node root = root_node(R);
+    int inserted = 0;
+    uint32_t* fin = M.fa;   // final record list
+    int nfin = 0;
+    const bool dbl = in.d0 == in.d1;
+    const int d = in.d0;
+
+    if (!dbl) {
+        // ------------------------------------------------ non-doubles
+        const int H = in.d0 > in.d1 ? in.d0 : in.d1, L = in.d0 > in.d1 ? in.d1 : in.d0;
+        const uint32_t okH = ok_mask(R.block, H, R.player), okL = ok_mask(R.block, L, R.player);
+        const Moves mH = node_moves(R, root, H, okH), mL = node_moves(R, root, L, okL);
+        const int pass = (l >> 4) & 1, k = l & 15;
+        const bool in32 = l < 32;
+        const int dA = pass ? L : H, dB = pass ? H : L;
+        const bool v1 = in32 && k < (pass ? mL.n : mH.n);
+        Moves mA;
+        mA.src = pass ? mL.src : mH.src;
+        mA.nsrc = pass ? mL.nsrc : mH.nsrc;
+        mA.e0 = pass ? mL.e0 : mH.e0;
+        mA.e1 = pass ? mL.e1 : mH.e1;
+        mA.n = pass ? mL.n : mH.n;
+        int s1 = 0;
+        if (v1) s1 = move_source(mA, k);
+        const Node child = v1 ? apply_move(R, root, s1, dA) : root;
+        Moves m2 = node_moves(R, child, dB, pass ? okH : okL);
+        const int c = v1 ? m2.n : 0;
+        const bool two1 = ballot(in32 && pass == 0 && c > 0) != 0ull;
+        const bool two2 = ballot(in32 && pass == 1 && c > 0) != 0ull;
+        const int nH = mH.n, nL = mL.n;
+        const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
+        const bool h1 = v1 && t1 < 24u && ((R.blot >> t1) & 1u);
+        if ((two1 || (nH != 1 && two2)) && nd_by_rule(R) && !(M.exp & 4)) {
+            // 2-move records without a table (nd_first): a pass-2 parent can
+            // only add its chain (s2 = t1) or reverse chain (s2 -> s1) child
+            if (pass == 1) {
+                const int rv = R.player == 0 ? s1 - H : s1 + H;
+                const uint32_t cand = (t1 < 24u ? 1u << t1 : 0u) | ((rv >= 0 && rv < 24) ? 1u << rv : 0u);
+                m2.src &= cand;
+                m2.nsrc = m2.n = __popc(m2.src);
+            }
+            const int cc = v1 ? m2.n : 0;
+            const uint32_t blot2 = R.blot & ~(h1 ? (1u << t1) : 0u);
+            const uint32_t occ0 = occ24(R.m0, R.m1, R.m2);
+            auto kfn = [&](int p, int s2) -> uint32_t {
+                const int ps1 = __shfl(s1, p, 64);
+                const int pt1 = __shfl((int)t1, p, 64);
+                const uint32_t pb2 = (uint32_t)__shfl((int)blot2, p, 64);
+                const bool ph1 = __shfl((int)h1, p, 64) != 0;
+                const int pp = p >> 4;
+                const int t2 = dest_of(R, s2, pp ? H : L);
+                const bool h2 = ((pb2 >> t2) & 1u) != 0u;
+                const uint32_t key = nd_key((uint32_t)ps1, (uint32_t)pt1, ph1, (uint32_t)s2, (uint32_t)t2, h2);
+                return nd_first(R, occ0, pp, ps1, pt1, s2, t2, H, L) ? key : ND_DROP;
+            };
+            if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin)) return -1;
+        } else if (two1 || (nH != 1 && two2)) {
+            // 2-move records in (pass, i, j) order (handle_non_doubles 43-68, both passes)
+            clear_tab<G>(M);
+            const int cc = in32 ? c : 0;
+            const uint32_t blot2 = R.blot & ~(h1 ? (1u << t1) : 0u);
+            auto kfn = [&](int p, int s2) -> uint32_t {
+                const uint32_t ps1 = (uint32_t)__shfl(s1, p, 64);
+                const uint32_t pt1 = (uint32_t)__shfl((int)t1, p, 64);
+                const uint32_t pb2 = (uint32_t)__shfl((int)blot2, p, 64);
+                const bool ph1 = __shfl((int)h1, p, 64) != 0;
+                const int pdB = (p >> 4) ? H : L;
+                const uint32_t t2 = (uint32_t)dest_of(R, s2, pdB);
+                const bool h2 = t2 < 24u && ((pb2 >> t2) & 1u);
+                return nd_key(ps1, pt1, ph1, (uint32_t)s2, t2, h2);
+            };
+            uint32_t tot;
+            if (!expand_flat<G>(M, m2, cc, 0u, 0u, kfn, fin, nfin, inserted, tot)) return -1;
+        } else {
+            // singles: high-die singles, then (unless pass 2 is skipped) low-die singles
+            // (handle_non_doubles 70-81; generate_all_moves.py:40-50)
+            clear_tab<G>(M);
+            const int nL2 = (nH == 1) ? 0 : nL;
+            const bool act = v1 && (pass == 0 || k < nL2);
+            const uint32_t ord = pass == 0 ? (uint32_t)k : (uint32_t)(nH + k);
+            const uint32_t key = nd_key((uint32_t)s1, t1, h1, 31u, 31u, false);
+            bool fresh;
+            const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
+            sync<G>();
+            const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
+            const uint64_t bm = ballot(sv);
+            if (sv) st32<G>(fin + mask_prefix(bm), key);
+            nfin = __popcll(bm);
+            sync<G>();
+        }
+    } else {
+        // ------------------------------------------------ doubles
+        const uint32_t okd = ok_mask(R.block, d, R.player);
+        uint32_t* fa = M.fa;
+        uint32_t* fb = M.fb;
+        if (doubles_by_path(R)) {
+            if (l == 0) st32<G>(fa, PATH_EMPTY);
+            sync<G>();
+            int n = 1, level = 0;
+            while (level < 4) {
+                int nn = 0;
+                uint32_t T = 0;
+                for (int b = 0; b < n; b += 64) {
+                    const int i = b + l;
+                    const bool live = i < n;
+                    const uint32_t path = live ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
+                    uint32_t bad;
+                    const Node nd = path_node(R, path, d, okd, bad);
+                    Moves pm = node_moves(R, nd, d, okd);
+                    const uint32_t one = pm.n == 1 ? FLAG1 : 0u;
+                    pm.src &= ~bad;                      // e0 is the bar entry (or none) here
+                    pm.nsrc = __popc(pm.src);
+                    const int c = live ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0;
+                    const int incl = wave_incl_scan(c);
+                    const int excl = incl - c;
+                    const int Tc = lane63(incl);
+                    if (n_out_check(nn, Tc, M.F)) return -1;
+                    for (int cb = 0; cb < Tc; cb += 64) {
+                        const int r = cb + l;
+                        const int p = flat_parent<G>(M.map, excl, c, cb);
+                        const int jj = r - __shfl(excl, p, 64);
+                        const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+                        const int nsrc = __shfl(pm.nsrc, p, 64);
+                        const int e0 = __shfl(pm.e0, p, 64);
+                        const uint32_t pp = (uint32_t)__shfl((int)path, p, 64);
+                        const uint32_t tag = (uint32_t)__shfl((int)one, p, 64);
+                        const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
+                        // append the step in the first empty field (level)
+                        const uint32_t child = (pp & ~(31u << (5 * level))) | ((uint32_t)sx << (5 * level));
+                        if (r < Tc) st32<G>(fb + nn + r, child | tag | PATHF);
+                    }
+                    nn += Tc;
+                    T += (uint32_t)Tc;
+                    if ((int)T > heavy_t) return -2;
+                }
+                sync<G>();
+                if (T == 0) break;
+                uint32_t* t = fa; fa = fb; fb = t;
+                n = nn;
+                ++level;
+            }
+            fin = fa;
+            if (level == 0) {
+                nfin = 0;
+            } else if (level == 4) {
+                nfin = n;
+            } else {
+                for (int b = 0; b < n; b += 64) {   // parent had one move (order kept)
+                    const int i = b + l;
+                    const uint32_t e = i < n ? ld32<G>(fa + i) : 0u;
+                    const bool rec = i < n && (e & FLAG1);
+                    const uint64_t bm = ballot(rec);
+                    sync<G>();
+                    if (rec) st32<G>(fa + nfin + mask_prefix(bm), e);
+                    nfin += __popcll(bm);
+                    sync<G>();
+                }
+            }
+            fin_out = fin;
+            return nfin;
+        }
+        if (l == 0) st32<G>(fa, KEY_EMPTY4);
+        sync<G>();
+        int n = 1, level = 0;
+        while (level < 4) {
+            clear_tab<G>(M);
+            inserted = 0;
+            int nn = 0;
+            uint32_t T = 0;
+            for (int b = 0; b < n; b += 64) {
+                const int i = b + l;
+                const bool live = i < n;
+                const uint32_t pkey = live ? ld32<G>(fa + i) & KEYMASK : KEY_EMPTY4;
+                const Moves pm = node_moves(R, rebuild(R, pkey, d), d, okd);
+                const int cnt = live ? pm.n : 0;
+                auto kfn = [&](int p, int s) -> uint32_t {
+                    return key_insert((uint32_t)__shfl((int)pkey, p, 64), rel_of(s, R.player));
+                };
+                uint32_t tot;
+                if (!expand_flat<G>(M, pm, cnt, pm.n == 1 ? FLAG1 : 0u, T, kfn, fb, nn, inserted, tot)) return -1;
+                T += tot;
+                if ((int)T > heavy_t) return -2;
+            }
+            if (T == 0) break;
+            uint32_t* t = fa; fa = fb; fb = t;
+            n = nn;
+            ++level;
+        }
+        // records: the deepest level; below depth 4 only nodes whose parent had one move
+        fin = fa;
+        if (level == 0) {
+            nfin = 0;
+        } else if (level == 4) {
+            nfin = n;
+        } else {
+            for (int b = 0; b < n; b += 64) {   // compact flagged nodes in place (order kept)
+                const int i = b + l;
+                const uint32_t e = i < n ? ld32<G>(fa + i) : 0u;
+                const bool rec = i < n && (e & FLAG1);
+                const uint64_t bm = ballot(rec);
+                sync<G>();
+                if (rec) st32<G>(fa + nfin + mask_prefix(bm), e);
+                nfin += __popcll(bm);
+                sync<G>();
+            }
+        }
+    }
+    fin_out = fin;
+    return nfin;
+}
+
+// write the job's records (keys in `fin`) as boards at rows base..base+nfin-1
+template <bool G>
+BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const uint32_t* fin, int nfin, int base) {
+    const bool dbl = in.d0 == in.d1;
+    for (int b = 0; b < nfin; b += 64) {
+        const int i = b + lane_id();
+        if (i < nfin) {
+            const uint32_t e = ld32<G>(fin + i);
+            const Node n = !dbl ? nd_board(in.R, e)
+                                : ((e & PATHF) ? path_board(in.R, e & KEYMASK, in.d0) : rebuild(in.R, e & KEYMASK, in.d0));
+            emit_one(a, j, in.R, n, i, base);
+        }
+    }
+}
+
+template <bool G>
+BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc,
+                    int heavy_t = 0x7FFFFFFF) {
+    uint32_t* fin = nullptr;
+    const int nfin = job_records<G>(in, M, fin, heavy_t);
+    if (nfin < 0) return nfin;
+    const int base = begin_emit(a, j, nfin, fc);
+    if (base >= 0 && !(M.exp & 1)) emit_records<G>(a, j, in, fin, nfin, base);
+    return nfin;
+}
+
+// ------------------------------------------------------------------ block-cooperative doubles
+// Small launches (no more jobs than resident waves, e.g. the 1-ply step) are
+// bound by their slowest job: a doubles roll with hundreds of results. A
+// doubles job whose level outgrows HEAVY_T children in its wave is expanded
+// again by the whole 16-wave block, level by level:
+//  1. parents (2 per thread): rebuild, move list -> LDS (src mask, packed
+//     extras, exclusive child prefix from a block scan), and a child -> parent
+//     map (u16 per child);
+//  2. children (one per thread per round): insert key << 32 | (ordinal << 1 |
+//     parent-had-one-move) into a table sized for the level (dedup_insert's
+//     CAS / atomicMin leave each key with its first-reach ordinal);
+//  3. survivors = the occupied slots: set bit[ordinal], prefix-popcount the
+//     bitmap, and each slot writes its key to the next frontier at its rank,
+//     i.e. in first-reach order.
+constexpr int BW = 16;                // waves per block
+constexpr int NTH = 64 * BW;          // threads per block
+constexpr int K_S = 4096;             // max table slots
+constexpr int K_F = 2 * NTH;          // frontier capacity (2 parents per thread)
+constexpr int K_TMAX = 16384;         // children per level
+constexpr int HEAVY_T = 128;             // measured: 256 / 128 / 64 -> 128 best (1-ply)
+struct CoopLds {
+    unsigned long long tab[K_S];
+    uint32_t fa[K_F], fb[K_F];
+    uint32_t psrc[K_F], ppack[K_F], pexcl[K_F];
+    uint16_t map[K_TMAX];
+    uint32_t bits[K_TMAX / 32];
+    uint16_t pre[K_TMAX / 32];
+    uint32_t wsum[BW];
+    uint32_t misc[8];                 // [0] inserted [1] record count [2] emit base [3] heavy mask
+};
+// block-wide exclusive scan of one value per thread; `total` = block sum
+BGX_DEV int block_excl_scan(CoopLds& C, int v, int& total) {
+    const int w = (int)threadIdx.x >> 6;
+    const int incl = wave_incl_scan(v);
+    if (lane_id() == 63) C.wsum[w] = (uint32_t)incl;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < BW; ++k) {
+        const int t = (int)C.wsum[k];
+        before += k < w ? t : 0;
+        total += t;
+    }
+    __syncthreads();
+    return before + incl - v;
+}
+
+// The table-free path expansion (doubles_by_path) by a whole block: per level
+// the parents' filtered move lists and child prefix, then one child per
+// thread written straight to its first-reach slot (no dedup, no ranking).
+BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
+    const Root& R = in.R;
+    const int d = in.d0;
+    const int t = (int)threadIdx.x, w = t >> 6;
+    const uint32_t okd = ok_mask(R.block, d, R.player);
+    uint32_t* fa = C.fa;
+    uint32_t* fb = C.fb;
+    if (t == 0) fa[0] = PATH_EMPTY;
+    __syncthreads();
+    int n = 1, level = 0;
+    while (level < 4) {
+        int c[2] = {0, 0};
+        uint32_t src[2] = {0u, 0u}, pack[2] = {0u, 0u};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            if (hh * NTH + 64 * w < n) {        // wave-uniform
+                const int i = hh * NTH + t;
+                const uint32_t path = i < n ? fa[i] & KEYMASK : PATH_EMPTY;
+                uint32_t bad;
+                const Moves pm = node_moves(R, path_node(R, path, d, okd, bad), d, okd);
+                const uint32_t ok = pm.src & ~bad;
+                const int ns = __popc(ok);
+                c[hh] = i < n ? ns + (pm.e0 >= 0 ? 1 : 0) : 0;
+                src[hh] = ok;
+                pack[hh] = (uint32_t)ns | ((uint32_t)(pm.e0 + 1) << 5) | (pm.n == 1 ? 1u << 15 : 0u);
+            }
+        }
+        int tot2;
+        const int ex2 = block_excl_scan(C, c[0] | (c[1] << 16), tot2);
+        const int T0 = tot2 & 0xFFFF, T = T0 + (tot2 >> 16);
+        if (T == 0) break;                      // uniform
+        if (T > K_F) return -1;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int i = hh * NTH + t;
+            if (i < n) {
+                const int ex = hh ? T0 + (ex2 >> 16) : (ex2 & 0xFFFF);
+                C.psrc[i] = src[hh];
+                C.ppack[i] = pack[hh];
+                C.pexcl[i] = (uint32_t)ex;
+                for (int k = 0; k < c[hh]; ++k) C.map[ex + k] = (uint16_t)i;
+            }
+        }
+        __syncthreads();
+        for (int r = t; r < T; r += NTH) {
+            const int p = (int)C.map[r];
+            const uint32_t pk = C.ppack[p];
+            const int jj = r - (int)C.pexcl[p];
+            const int nsrc = (int)(pk & 31u);
+            const int sx = jj < nsrc ? select_bit_fast(C.psrc[p], jj) : (int)((pk >> 5) & 31u) - 1;
+            const uint32_t pp = fa[p] & KEYMASK;
+            const uint32_t child = (pp & ~(31u << (5 * level))) | ((uint32_t)sx << (5 * level));
+            fb[r] = child | (((pk >> 15) & 1u) ? FLAG1 : 0u) | PATHF;
+        }
+        __syncthreads();
+        uint32_t* tmp = fa; fa = fb; fb = tmp;
+        n = T;
+        ++level;
+    }
+    fin = fa;
+    if (level == 4) return n;
+    if (level == 0) return 0;
+    const int i0 = 2 * t;
+    const uint32_t e0 = i0 < n ? fa[i0] : 0u, e1 = i0 + 1 < n ? fa[i0 + 1] : 0u;
+    const int f0 = (i0 < n && (e0 & FLAG1)) ? 1 : 0, f1 = (i0 + 1 < n && (e1 & FLAG1)) ? 1 : 0;
+    int nf;
+    const int pos = block_excl_scan(C, f0 + f1, nf);
+    if (f0) fb[pos] = e0;
+    if (f1) fb[pos + f0] = e1;
+    __syncthreads();
+    fin = fb;
+    return nf;
+}
+
+// returns the record count (records in `fin`), -1 = overflow (tier 3)
+BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin) {
+    if (doubles_by_path(in.R)) return coop_doubles_path(in, C, fin);
+    const Root& R = in.R;
+    const int d = in.d0;
+    const int t = (int)threadIdx.x, l = lane_id();
+    const uint32_t okd = ok_mask(R.block, d, R.player);
+    uint32_t* fa = C.fa;
+    uint32_t* fb = C.fb;
+    if (t == 0) fa[0] = KEY_EMPTY4;
+    __syncthreads();
+    int n = 1, level = 0;
+    while (level < 4) {
+        // 1. parents t and t + NTH (waves past the level skip the work)
+        const int w = t >> 6;
+        int c[2] = {0, 0};
+        uint32_t src[2] = {0u, 0u}, pack[2] = {0u, 0u};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            if (hh * NTH + 64 * w < n) {        // wave-uniform
+                const int i = hh * NTH + t;
+                const uint32_t pkey = i < n ? fa[i] & KEYMASK : KEY_EMPTY4;
+                const Moves pm = node_moves(R, rebuild(R, pkey, d), d, okd);
+                c[hh] = i < n ? pm.n : 0;
+                src[hh] = pm.src;
+                pack[hh] = (uint32_t)pm.nsrc | ((uint32_t)(pm.e0 + 1) << 5) | ((uint32_t)(pm.e1 + 1) << 10) |
+                           (pm.n == 1 ? 1u << 15 : 0u);
+            }
+        }
+        // one block scan of both halves (16-bit fields: T <= K_TMAX < 2^15)
+        int tot2;
+        const int ex2 = block_excl_scan(C, c[0] | (c[1] << 16), tot2);
+        const int T0 = tot2 & 0xFFFF, T = T0 + (tot2 >> 16);
+        if (T == 0) break;                      // uniform
+        if (T > K_TMAX) return -1;
+        int S = 64;
+        while (S < 2 * T && S < K_S) S <<= 1;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int i = hh * NTH + t;
+            if (i < n) {
+                const int ex = hh ? T0 + (ex2 >> 16) : (ex2 & 0xFFFF);
+                C.psrc[i] = src[hh];
+                C.ppack[i] = pack[hh];
+                C.pexcl[i] = (uint32_t)ex;
+                for (int k = 0; k < c[hh]; ++k) C.map[ex + k] = (uint16_t)i;
+            }
+        }
+        for (int i = t; i < S; i += NTH) C.tab[i] = EMPTY64;
+        const int nwd = (T + 31) >> 5;
+        for (int i = t; i < nwd; i += NTH) C.bits[i] = 0u;
+        if (t == 0) C.misc[0] = 0u;
+        __syncthreads();
+        // 2. children
+        Mem M;
+        M.tab = C.tab;
+        M.S = S;
+        int fresh_n = 0;
+        for (int b = 0; b < T; b += NTH) {     // uniform trip count
+            if (b + 64 * w >= T) break;        // wave-uniform: no children left for this wave
+            const int r = b + t;
+            const bool act = r < T;
+            const int p = act ? (int)C.map[r] : 0;
+            const uint32_t pk = C.ppack[p];
+            const int jj = r - (int)C.pexcl[p];
+            const int nsrc = (int)(pk & 31u);
+            const int sx = jj < nsrc ? select_bit_fast(C.psrc[p], jj)
+                                     : (jj == nsrc ? (int)((pk >> 5) & 31u) - 1 : (int)((pk >> 10) & 31u) - 1);
+            const uint32_t key = key_insert(fa[p] & KEYMASK, rel_of(sx, R.player));
+            const uint32_t ordw = ((uint32_t)r << 1) | ((pk >> 15) & 1u);
+            bool fresh;
+            dedup_insert<false>(M, act, key, ordw, fresh);
+            fresh_n += __popcll(ballot(fresh));
+        }
+        if (l == 0 && fresh_n) atomicAdd(&C.misc[0], (uint32_t)fresh_n);
+        __syncthreads();
+        if ((int)C.misc[0] > K_F) return -1;   // uniform
+        // 3. survivors in ordinal order
+        for (int i = t; i < S; i += NTH) {
+            const unsigned long long v = C.tab[i];
+            if (v != EMPTY64) {
+                const uint32_t o = (uint32_t)v >> 1;
+                atomicOr(&C.bits[o >> 5], 1u << (o & 31));
+            }
+        }
+        __syncthreads();
+        int nn;
+        const int cw = t < nwd ? __popc(C.bits[t]) : 0;   // nwd <= K_TMAX / 32 = NTH / 2
+        const int pw = block_excl_scan(C, cw, nn);
+        if (t < nwd) C.pre[t] = (uint16_t)pw;
+        __syncthreads();
+        for (int i = t; i < S; i += NTH) {
+            const unsigned long long v = C.tab[i];
+            if (v != EMPTY64) {
+                const uint32_t ow = (uint32_t)v, o = ow >> 1;
+                const int rank = (int)C.pre[o >> 5] + __popc(C.bits[o >> 5] & ((1u << (o & 31)) - 1u));
+                fb[rank] = (uint32_t)(v >> 32) | ((ow & 1u) ? FLAG1 : 0u);
+            }
+        }
+        __syncthreads();
+        uint32_t* tmp = fa; fa = fb; fb = tmp;
+        n = nn;
+        ++level;
+    }
+    fin = fa;
+    if (level == 4) return n;
+    if (level == 0) return 0;
+    // below depth 4: only nodes whose parent had one move (order kept)
+    const int i0 = 2 * t;
+    const uint32_t e0 = i0 < n ? fa[i0] : 0u, e1 = i0 + 1 < n ? fa[i0 + 1] : 0u;
+    const int f0 = (i0 < n && (e0 & FLAG1)) ? 1 : 0, f1 = (i0 + 1 < n && (e1 & FLAG1)) ? 1 : 0;
+    int nf;
+    const int pos = block_excl_scan(C, f0 + f1, nf);
+    if (f0) fb[pos] = e0;
+    if (f1) fb[pos + f0] = e1;
+    __syncthreads();
+    fin = fb;
+    return nf;
+}
+
+// ------------------------------------------------------------------ kernels
+template <int S>
+BGX_DEV Mem lds_mem(unsigned long long* smem) {
+    Mem M;
+    M.tab = smem;
+    M.F = Slice<S>::F;
+    M.fa = (uint32_t*)(smem + S);
+    M.fb = M.fa + M.F;
+    M.map = M.fb + M.F;
+    M.S = S;
+    M.map[lane_id()] = 0u;
+    wave_sync();
+    return M;
+}
+
+BGX_DEV void push_ovf(const MovegenArgs& a, int j) {
+    const unsigned slot = atomicAdd(a.ovf_count, 1u);
+    if ((int)slot < a.ovf_cap) a.ovf_list[slot] = j;
+    else atomicOr(a.err_flags, BGX_ERRF_OVF_LIST);
+}
+
+}  // namespace bgx

@@ -197,7 +197,7 @@ def test_graph_launch_matches_direct_launch(ply, monkeypatch):
     runs = []
     for g in ("1", "0"):
         monkeypatch.setenv("BGX_GRAPH", g)
-        e = _engine(w, lanes=256, seed=11, ply=ply, k_top=4)
+        e = _engine(w, lanes=256, seed=11, ply=ply, k_top=4, fused=False)
         runs.append(_by_episode(*_collect(e, 120 if ply == 1 else 40, chunk=40)))
         e.close()
     a, b = runs
@@ -257,3 +257,47 @@ def test_engine_greedy_picks_the_highest_value(weights_ckpt):
             assert v[a] >= v.max() - V_TOL, (k, a, v[a], v.max())
             n += 1
     assert n > 2000
+
+
+def _same_runs(a, b):
+    assert len(a) > 0 and a.keys() == b.keys()
+    for key in a:
+        np.testing.assert_array_equal(a[key][0], b[key][0], err_msg=str(key))
+        for f in a[key][1]:
+            np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")
+
+
+@pytest.mark.parametrize("tier", ["", "2", "3"])
+def test_fused_step_matches_phased_engine(weights_seed0, tier, monkeypatch):
+    """The fused 1-ply kernel (one persistent launch per step() call, 16 lanes
+    per workgroup) and the phased engine (movegen / MLP / select launches per
+    step) produce identical episodes and records for the same seed: same
+    afterstates in the same order, V with the same bits, same samples. With
+    BGX_MG_TEST_TIER=2/3 every fused movegen job is redone by the workgroup
+    tiers (cooperative doubles / 32 KB slice, or the global workspace)."""
+    lanes, steps = (300, 160) if not tier else (48, 60)
+    ref = _engine(weights_seed0, lanes=lanes, seed=17, ply=1, fused=False)
+    a = _by_episode(*_collect(ref, steps, chunk=40))
+    ref.close()
+    if tier:
+        monkeypatch.setenv("BGX_MG_TEST_TIER", tier)
+    e = _engine(weights_seed0, lanes=lanes, seed=17, ply=1, fused=True)
+    assert e.fused
+    b = _by_episode(*_collect(e, steps, chunk=40))
+    st = e.stats()
+    e.close()
+    _same_runs(a, b)
+    assert st["env_steps"] == lanes * steps
+    if tier:
+        assert st["fallback_jobs"] > 0
+
+
+def test_fused_greedy_and_ragged_lanes(weights_ckpt):
+    """A lane count that is not a multiple of 16 (the last workgroup is partly
+    empty) and greedy play: fused == phased on the shipped checkpoint."""
+    runs = []
+    for fused in (False, True):
+        e = _engine(weights_ckpt, lanes=37, seed=9, ply=1, greedy=True, fused=fused)
+        runs.append(_by_episode(*_collect(e, 200, chunk=50)))
+        e.close()
+    _same_runs(*runs)
