@@ -151,6 +151,7 @@ struct bgx_engine {
     uint32_t* fcand = nullptr;
     float* fvbuf = nullptr;
     int fcap = 0;
+    unsigned long long* fprof = nullptr;   // BGX_FUSED_PROF: phase clocks, printed at destroy
     // harvest
     uint32_t* out_records = nullptr;
     int out_cap = 0;
@@ -405,6 +406,23 @@ int bgx_engine_destroy(bgx_engine* e) {
     if (!e) return BGX_OK;
     hipSetDevice(e->device);
     hipDeviceSynchronize();
+    if (e->fprof) {   // development report (BGX_FUSED_PROF): per workgroup-step averages, wall clock 100 MHz
+        std::vector<unsigned long long> p((size_t)1024 * 16);
+        if (hipMemcpy(p.data(), e->fprof, p.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            double s[12] = {0};
+            for (int b = 0; b < 1024; ++b)
+                for (int k = 0; k < 11; ++k) s[k] += (double)p[(size_t)b * 16 + k];
+            const double n = s[5] > 0 ? s[5] : 1;
+            fprintf(stderr, "[bgx fused prof] us per workgroup step: tier1 %.2f tier2 %.2f wload %.2f mlp %.2f "
+                    "select+step %.2f | mean wave tier-1 job %.2f (%0.f workgroup steps)\n",
+                    s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n / 100, s[4] / n / 100,
+                    s[6] / n / 16 / 100, n);
+            fprintf(stderr, "[bgx fused prof] mean per wave-step: mlp tiles %.2f | select: V fill %.2f pick %.2f "
+                    "advance %.2f us\n", s[7] / n / 16 / 100, s[8] / n / 16 / 100, s[9] / n / 16 / 100,
+                    s[10] / n / 16 / 100);
+        }
+        hipFree(e->fprof);
+    }
     void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
                   e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
                   e->d_offs, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
@@ -682,6 +700,14 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.ws_slots = e->ws_slots;
     f.ws_words_per_block = (size_t)5 * e->ws_slots;
     if (const char* v = getenv("BGX_MG_TEST_TIER")) f.force_tier = atoi(v);
+    if (const char* v = getenv("BGX_FUSED_EXP")) f.exp = atoi(v);
+    if (getenv("BGX_FUSED_PROF")) {
+        if (!e->fprof) {
+            if (dalloc(&e->fprof, (size_t)1024 * 16)) return BGX_E_HIP;
+            HIP_TRY(hipMemset(e->fprof, 0, (size_t)1024 * 16 * 8));
+        }
+        f.prof = e->fprof;
+    }
     if (timed(e, 0, s, true)) return BGX_E_HIP;
     HIP_TRY(bgx_launch_fused(&f, s));
     if (timed(e, 0, s, false)) return BGX_E_HIP;

@@ -309,6 +309,36 @@ BGX_DEV int wave_incl_max(int v) {   // v >= 0
     return v;
 }
 BGX_DEV int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
+BGX_DEV float lane63f(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+// float versions (DPP, VALU latency instead of ds_bpermute shuffles)
+template <int CTRL, int ROW_MASK>
+BGX_DEV float dpp_addf(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, CTRL < 0x140));
+}
+template <int CTRL, int ROW_MASK>
+BGX_DEV float dpp_maxf(float v) {   // lanes without a source keep -inf
+    const float t = __int_as_float(
+        __builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+    return fmaxf(v, t);
+}
+BGX_DEV float wave_incl_scanf(float v) {
+    v = dpp_addf<0x111, 0xF>(v);
+    v = dpp_addf<0x112, 0xF>(v);
+    v = dpp_addf<0x114, 0xF>(v);
+    v = dpp_addf<0x118, 0xF>(v);
+    v = dpp_addf<0x142, 0xA>(v);
+    v = dpp_addf<0x143, 0xC>(v);
+    return v;
+}
+BGX_DEV float wave_incl_maxf(float v) {
+    v = dpp_maxf<0x111, 0xF>(v);
+    v = dpp_maxf<0x112, 0xF>(v);
+    v = dpp_maxf<0x114, 0xF>(v);
+    v = dpp_maxf<0x118, 0xF>(v);
+    v = dpp_maxf<0x142, 0xA>(v);
+    v = dpp_maxf<0x143, 0xC>(v);
+    return v;
+}
 BGX_DEV int wave_sum(int v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

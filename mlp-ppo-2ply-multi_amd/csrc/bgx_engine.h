@@ -117,107 +117,141 @@ BGX_DEV Outcome judge(const uint32_t* w, int pl, uint32_t& flags) {
 }
 
 
+// A lane's state between env steps (EngineDev SoA fields of lane i).
+struct LaneState {
+    uint32_t w[8];        // board, indicator flag = player to move
+    int p, d0, d1, steps;
+    uint32_t flags, epi, rec, ep_first, harv;
+    uint64_t ctr;         // Philox counter
+};
+BGX_DEV void lane_load(const EngineDev& e, int i, LaneState& s) {
+    load_packed(e.rows + (size_t)i * 8, s.w);
+    s.p = e.player[i];
+    s.d0 = e.dice[2 * i];
+    s.d1 = e.dice[2 * i + 1];
+    s.steps = e.step[i];
+    s.flags = e.flags[i];
+    s.epi = e.epi[i];
+    s.rec = e.rec_count[i];
+    s.ep_first = e.ep_first[i];
+    s.harv = e.harv[i];
+    s.ctr = e.rng[i];
+}
+// everything but the board row (lane_advance writes that every step)
+BGX_DEV void lane_store(const EngineDev& e, int i, const LaneState& s) {
+    e.player[i] = (uint8_t)s.p;
+    e.dice[2 * i] = (uint8_t)s.d0;
+    e.dice[2 * i + 1] = (uint8_t)s.d1;
+    e.step[i] = s.steps;
+    e.flags[i] = s.flags;
+    e.epi[i] = s.epi;
+    e.rec_count[i] = s.rec;
+    e.ep_first[i] = s.ep_first;
+    e.rng[i] = s.ctr;
+}
+
 // One game lane's env step after its action is chosen (BackgammonEnv.step,
 // backgammon_env.py:130-221, + the worker's Experience, worker.py:101-162):
 // apply, judge, record, and on game end append the episode header and reset.
-// action < 0 (or no legal move): pass.
-// `chosen` = the packed row of candidate `action`, vs / va = V(s) / V(a),
-// n_full = the full candidate count (the phased engine's rows, or the fused
-// kernel's per-lane candidate slots).
-BGX_DEV void step_lane_core(const EngineDev& e, int i, int action, const uint32_t* chosen, float vs, float va,
-                            int n_full) {
-    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), e.rng[i]};
-    int p = e.player[i];
-    int steps = e.step[i];
-    uint32_t flags = e.flags[i];
-    uint32_t w[8];
-    load_packed(e.rows + (size_t)i * 8, w);
+// action < 0 (or no legal move): pass. `chosen` = the packed row of candidate
+// `action`, vs / va = V(s) / V(a), n_full = the full candidate count. The
+// state update runs on every calling thread (a wave keeps its lane's state
+// uniform in registers); only `lead` writes memory (record, episode header,
+// the lane's board row).
+BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, int action, const uint32_t* chosen, float vs,
+                          float va, int n_full, bool lead) {
+    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), s.ctr};
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
-    int d0 = e.dice[2 * i], d1 = e.dice[2 * i + 1];
     bool done = false;
     int win_type = 0, winner = -1;
     if (n == 0 || action < 0) {
         // pass (backgammon_env.py:139-151): no experience is recorded (worker.py:106-113)
-        p ^= 1;
-        rng.roll(d0, d1);
+        s.p ^= 1;
+        rng.roll(s.d0, s.d1);
     } else {
-        flags |= 16u << p;
-        rng.ctr++;   // the select kernel's sampling uniform
+        s.flags |= 16u << s.p;
+        rng.ctr++;   // the sampling uniform (lane_uniform)
         const int a = action;
         uint32_t nb[8];
         load_packed(chosen, nb);
-        const int mover = p;
-        const Outcome o = judge(nb, mover, flags);
+        const int mover = s.p;
+        const int dd0 = s.d0, dd1 = s.d1;
+        const Outcome o = judge(nb, mover, s.flags);
         done = o.done;
         if (done) { win_type = o.win_type; winner = mover; }
-        else { p ^= 1; rng.roll(d0, d1); }
+        else { s.p ^= 1; rng.roll(s.d0, s.d1); }
         // experience record (worker.py:149-156; Experience, episode.py:5-46)
-        const uint32_t rec = e.rec_count[i];
-        if (rec - e.harv[i] >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
-        uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
-        uint32_t before[8];
-        for (int k = 0; k < 8; ++k) before[k] = w[k];
-        set_flag(before, mover);
-        set_flag(nb, done ? mover : p);
-        store_packed(R, before);
-        store_packed(R + 8, nb);
-        const int dd0 = e.dice[2 * i], dd1 = e.dice[2 * i + 1];
-        uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
-                                 (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
-        uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
-                                     ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
-                                     ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
-                                 e.epi[i], (uint32_t)steps, (uint32_t)(e.lane_base + i));
-        ((uint4*)(R + 16))[0] = tail0;
-        ((uint4*)(R + 16))[1] = tail1;
-        e.rec_count[i] = rec + 1;
-        for (int k = 0; k < 8; ++k) w[k] = nb[k];
-    }
-    ++steps;
-    set_flag(w, p);
-    if (done || steps >= e.max_steps) {
-        const uint32_t slot = atomicAdd(e.ep_count, 1u);
-        if ((int)slot < e.ep_cap) {
-            uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
-            const uint32_t first = e.ep_first[i], nrec = e.rec_count[i] - first;
-            ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), e.epi[i], first, nrec);
-            ((uint4*)h)[1] = make_uint4((uint32_t)steps,
-                                        (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
-                                            (flags << 16),
-                                        0u, 0u);
-        } else {
-            atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
+        const uint32_t rec = s.rec;
+        if (lead) {
+            if (rec - s.harv >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
+            uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
+            uint32_t before[8];
+            for (int k = 0; k < 8; ++k) before[k] = s.w[k];
+            set_flag(before, mover);
+            uint32_t after[8];
+            for (int k = 0; k < 8; ++k) after[k] = nb[k];
+            set_flag(after, done ? mover : s.p);
+            store_packed(R, before);
+            store_packed(R + 8, after);
+            uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
+                                     (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
+            uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
+                                         ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
+                                         ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
+                                     s.epi, (uint32_t)s.steps, (uint32_t)(e.lane_base + i));
+            ((uint4*)(R + 16))[0] = tail0;
+            ((uint4*)(R + 16))[1] = tail1;
         }
-        p = new_game(rng, w, d0, d1);
-        steps = 0;
-        flags = 0;
-        e.epi[i] = e.epi[i] + 1;
-        e.ep_first[i] = e.rec_count[i];
+        s.rec = rec + 1;
+        for (int k = 0; k < 8; ++k) s.w[k] = nb[k];
     }
-    store_packed(e.rows + (size_t)i * 8, w);
-    e.player[i] = (uint8_t)p;
-    e.dice[2 * i] = (uint8_t)d0;
-    e.dice[2 * i + 1] = (uint8_t)d1;
-    e.step[i] = steps;
-    e.flags[i] = flags;
-    e.rng[i] = rng.ctr;
+    ++s.steps;
+    set_flag(s.w, s.p);
+    if (done || s.steps >= e.max_steps) {
+        if (lead) {
+            const uint32_t slot = atomicAdd(e.ep_count, 1u);
+            if ((int)slot < e.ep_cap) {
+                uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
+                const uint32_t first = s.ep_first, nrec = s.rec - first;
+                ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), s.epi, first, nrec);
+                ((uint4*)h)[1] = make_uint4((uint32_t)s.steps,
+                                            (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
+                                                (s.flags << 16),
+                                            0u, 0u);
+            } else {
+                atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
+            }
+        }
+        s.p = new_game(rng, s.w, s.d0, s.d1);
+        s.steps = 0;
+        s.flags = 0;
+        s.epi = s.epi + 1;
+        s.ep_first = s.rec;
+    }
+    if (lead) store_packed(e.rows + (size_t)i * 8, s.w);
+    s.ctr = rng.ctr;
 }
 
-// the phased engine's lane step: candidates at rows L + cand_off[i] + k, V in e.V
+// the phased engine's lane step: candidates at rows L + cand_off[i] + k, V in
+// e.V; the lane's state from and back to memory (one thread)
 BGX_DEV void step_lane(const EngineDev& e, int i, int action) {
     const int n_full = e.cand_cnt[i];
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
     const int base = e.L + e.cand_off[i];
     const bool act = n > 0 && action >= 0;
-    step_lane_core(e, i, action, e.rows + (size_t)(base + (act ? action : 0)) * 8, e.V[i],
-                   act ? e.V[base + action] : 0.0f, n_full);
+    LaneState s;
+    lane_load(e, i, s);
+    lane_advance(e, i, s, action, e.rows + (size_t)(base + (act ? action : 0)) * 8, e.V[i],
+                 act ? e.V[base + action] : 0.0f, n_full, true);
+    lane_store(e, i, s);
 }
 
-// The lane's sampling uniform: Philox at its current counter (step_lane_core
+// The lane's sampling uniform: Philox at its counter `ctr` (lane_advance
 // advances the counter past it).
-BGX_DEV float lane_uniform(const EngineDev& e, int i) {
-    return unit_from(philox(lane_key(e.seed, (uint32_t)(e.lane_base + i)), 0x5EED0000ull, e.rng[i]).x);
+BGX_DEV float lane_uniform(const EngineDev& e, int i, uint64_t ctr) {
+    return unit_from(philox(lane_key(e.seed, (uint32_t)(e.lane_base + i)), 0x5EED0000ull, ctr).x);
 }
+BGX_DEV float lane_uniform(const EngineDev& e, int i) { return lane_uniform(e, i, e.rng[i]); }
 
 // Action choice over the scores x[0..m) (wave-private LDS, m >= 1) by one
 // wavefront: softmax(x) + inverse-CDF sample at uniform u (worker.py:137-143,
@@ -227,12 +261,10 @@ BGX_DEV int pick_action(const float* x, int m, bool greedy, float u) {
     const int l = lane_id();
     float mx = -INFINITY;
     for (int k = l; k < m; k += 64) mx = fmaxf(mx, x[k]);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    mx = lane63f(wave_incl_maxf(mx));
     float sum = 0.0f;
     for (int k = l; k < m; k += 64) sum += __expf(x[k] - mx);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    sum = lane63f(wave_incl_scanf(sum));
     if (greedy) {
         float bv = -INFINITY;
         int bk = 0x7FFFFFFF;
@@ -251,19 +283,13 @@ BGX_DEV int pick_action(const float* x, int m, bool greedy, float u) {
     float carry = 0.0f;
     for (int b = 0; b < m; b += 64) {
         const int k = b + l;
-        float p = k < m ? __expf(x[k] - mx) : 0.0f;
-        // inclusive scan of p over the wave
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const float q = __shfl_up(p, off, 64);
-            if (l >= off) p += q;
-        }
+        const float p = wave_incl_scanf(k < m ? __expf(x[k] - mx) : 0.0f);   // inclusive scan over the wave
         const uint64_t hit = ballot(k < m && t < carry + p);
         if (hit) {
             pick = b + __ffsll((unsigned long long)hit) - 1;
             break;
         }
-        carry += __shfl(p, 63, 64);
+        carry += lane63f(p);
     }
     return pick;
 }

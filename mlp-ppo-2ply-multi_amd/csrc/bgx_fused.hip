@@ -10,10 +10,11 @@
 //   2. the LDS that held the slices now takes the split-fp16 W fragments;
 //   3. value MLP over the workgroup's rows (the lanes' obs rows + candidates,
 //      ~350 per step) in 32-board MFMA tiles spread over the 16 waves
-//      (mlp_tile_value: the mlp_kernel<1, NW> sequence, so V has the same bits
-//      as the phased engine's);
+//      (mlp_item: one (tile, m-tile) per wave at a time, partials summed in the
+//      canonical order, so V has the same bits as the phased engine's);
 //   4. each wave samples its lane's action from softmax(V/T) and lane 0 runs
-//      the env step (step_lane_core: apply, rewards, record, reset).
+//      the env step (lane_advance: apply, rewards, record, reset) on the
+//      lane's state, which stays in the wave's registers for the whole launch.
 // Replaces, per lane and step, Worker.play_episode's inner loop
 // (src/multi/worker.py:101-162) over BackgammonEnv.step / update_legal_moves
 // (src/environments/backgammon_env.py:130-308) and the policy forward
@@ -38,9 +39,14 @@ struct FusedTail {
     float w2s[128];                 // value-head weights
     int cnt[FW];                    // lane's full candidate count this step (-1: redo in tier 2)
     int pre[FW + 1];                // MLP row prefix over the lanes
+    uint32_t job[FW][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
+    LaneState st[FW];               // the lanes' state for the whole launch (written back at the end)
 };
 constexpr int F_LDS = F_OVL + (int)sizeof(FusedTail);
+constexpr int FT = (F_OVL - NFRAG * 16) / (4 * 64 * 4 + 32 * 32);   // MLP tiles per batch: partials + rows after W
+static_assert(FT >= 4, "partials fit behind W");
 
+template <bool PROF>
 __global__ __launch_bounds__(64 * FW) void fused_step_kernel(FusedArgs f) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     uint8_t* lds = (uint8_t*)smem;
@@ -51,10 +57,6 @@ __global__ __launch_bounds__(64 * FW) void fused_step_kernel(FusedArgs f) {
     for (int i = t; i < 128; i += 64 * FW) T.w2s[i] = f.rowc[i];
 
     MovegenArgs a{};
-    a.in_mode = IN_PACKED;
-    a.in_packed = e.rows;
-    a.in_player = e.player;
-    a.in_dice = e.dice;
     a.out_mode = OUT_PACKED_SLOT;
     a.cap = f.cap;
     a.out_packed = f.cand;
@@ -67,14 +69,30 @@ __global__ __launch_bounds__(64 * FW) void fused_step_kernel(FusedArgs f) {
     a.err_flags = e.err_flags;
 
     unsigned long long n_rows = 0, n_fb = 0, n_steps = 0;
+    // development timers (f.prof): phase sums on thread 0, tier-1 job time per wave
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tj = 0, tc = 0, tw[4] = {0, 0, 0, 0};
+    constexpr bool prof = PROF;
+    auto tick = [&](int k) {
+        if (prof && t == 0) {
+            const unsigned long long c = wall_clock64();
+            ph[k] += c - tc;
+            tc = c;
+        }
+    };
     const int groups = (e.L + FW - 1) / FW;
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int i = g * FW + w;   // this wave's lane
         const bool live = i < e.L;
+        // the lane's state stays in LDS for all n_steps (every lane of the wave
+        // computes the same update; lane 0 writes memory)
+        LaneState& st = T.st[w];
+        if (live) lane_load(e, i, st);
         n_steps += (unsigned long long)(e.L - g * FW < FW ? e.L - g * FW : FW) * (unsigned long long)f.n_steps;
         for (int step = 0; step < f.n_steps; ++step) {
             // ---- 1. tier-1 movegen in the wave's slice
+            if (prof && t == 0) tc = wall_clock64();
             {
+                const unsigned long long j0 = prof ? wall_clock64() : 0ull;
                 unsigned long long* sl = smem + (size_t)w * (Slice<S_T1>::bytes / 8);
                 Mem M;
                 M.tab = sl;
@@ -87,20 +105,27 @@ __global__ __launch_bounds__(64 * FW) void fused_step_kernel(FusedArgs f) {
                 wave_sync();
                 int nf = 0;
                 if (live) {
-                    const JobIn in = fetch_job(a, i);
+                    if (l < 8)
+                        T.job[w][l] = l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
+                    const JobIn in = make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6], st.p,
+                                              st.d0, st.d1);
                     uint32_t* fin = nullptr;
                     nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, 0x7FFFFFFF);
                     if (nf >= 0) emit_records<false>(a, i, in, fin, nf, 0);
                 }
                 if (l == 0) T.cnt[w] = nf;
+                if (prof) tj += wall_clock64() - j0;
             }
             __syncthreads();
+            tick(0);
             // ---- 1b. jobs that outgrew their slice: the whole workgroup, one at a time
             for (int v = 0; v < FW; ++v) {
                 if (T.cnt[v] >= 0) continue;   // uniform: LDS after a barrier
                 ++n_fb;
                 const int j = g * FW + v;
-                const JobIn in = fetch_job(a, j);
+                const uint32_t* q = T.job[v];
+                const JobIn in = make_job(q[0], q[1], q[2], q[3], q[4], q[5], q[6], (int)(q[7] & 255u),
+                                          (int)((q[7] >> 8) & 255u), (int)(q[7] >> 16));
                 FlatCursor fc;
                 auto run_global = [&]() -> int {
                     uint32_t* base = f.ws_global + (size_t)blockIdx.x * f.ws_words_per_block;
@@ -145,6 +170,7 @@ __global__ __launch_bounds__(64 * FW) void fused_step_kernel(FusedArgs f) {
                 }
                 __syncthreads();
             }
+            tick(1);
             // ---- 2. row prefix (lanes that pass evaluate nothing) + W fragments into the overlay
             if (t == 0) {
                 int acc = 0;
@@ -158,48 +184,112 @@ __global__ __launch_bounds__(64 * FW) void fused_step_kernel(FusedArgs f) {
             uint4* wf = (uint4*)lds;
             for (int k = t; k < NFRAG; k += 64 * FW) wf[k] = f.wfrag[k];
             __syncthreads();
-            // ---- 3. value MLP over the workgroup's rows, 32-board tiles
+            tick(2);
+            // ---- 3. value MLP over the workgroup's rows: (32-board tile, m-tile)
+            // items spread over the 16 waves, partials combined in the
+            // canonical epilogue order (bgx_mlp.h); batches of FT tiles
             const int nr = T.pre[FW];
             n_rows += (unsigned long long)nr;
-            for (int tile = w; tile * 32 < nr; tile += FW) {
-                const int r = tile * 32 + (l & 31);
-                uint4 bx = make_uint4(0, 0, 0, 0), by = make_uint4(0, 0, 0, 0);
-                size_t dst = ~(size_t)0;
-                if (r < nr) {
-                    int v = 0;
+            const unsigned long long m0 = prof ? wall_clock64() : 0ull;
+            // row r of the workgroup -> its packed board / its V slot
+            auto lane_of = [&](int r) -> int {
+                int v = 0;
 #pragma unroll
-                    for (int q = 1; q < FW; ++q) v += T.pre[q] <= r ? 1 : 0;
-                    const int k = r - T.pre[v];
-                    const int li = g * FW + v;
-                    const uint32_t* src =
-                        k == 0 ? e.rows + (size_t)li * 8 : f.cand + ((size_t)li * f.cap + (k - 1)) * 8;
-                    bx = ((const uint4*)src)[0];
-                    by = ((const uint4*)src)[1];
-                    dst = (size_t)li * (f.cap + 1) + k;
+                for (int q = 1; q < FW; ++q) v += T.pre[q] <= r ? 1 : 0;
+                return v;
+            };
+            auto row_of = [&](int r, uint4& bx, uint4& by) {
+                const int v = lane_of(r), k = r - T.pre[v];
+                const int li = g * FW + v;
+                const uint32_t* src =
+                    k == 0 ? e.rows + (size_t)li * 8 : f.cand + ((size_t)li * f.cap + (k - 1)) * 8;
+                bx = ((const uint4*)src)[0];
+                by = ((const uint4*)src)[1];
+            };
+            auto vslot = [&](int r) -> size_t {
+                const int v = lane_of(r), k = r - T.pre[v];
+                return (size_t)(g * FW + v) * (f.cap + 1) + k;
+            };
+            // batch of FT tiles: rows staged in LDS (one global load per row, all
+            // in flight together), then the items, then the combine
+            float* vp = (float*)(lds + NFRAG * 16);                 // [4][FT][64] partials
+            uint4* rs = (uint4*)(lds + NFRAG * 16 + 4 * FT * 64 * 4);   // [FT * 32][2] staged rows
+            const int n_tiles = (nr + 31) >> 5;
+            for (int tb = 0; tb < n_tiles; tb += FT) {
+                const int nt = n_tiles - tb < FT ? n_tiles - tb : FT;
+                if (tb > 0) __syncthreads();   // the previous batch's rows / partials are consumed
+                for (int c = t; c < nt * 32; c += 64 * FW) {
+                    const int r = tb * 32 + c;
+                    uint4 bx = make_uint4(0, 0, 0, 0), by = make_uint4(0, 0, 0, 0);
+                    if (r < nr) row_of(r, bx, by);
+                    rs[2 * c] = bx;
+                    rs[2 * c + 1] = by;
                 }
-                const float val = mlp_tile_value_m(wf, T.lut, T.w2s, f.feat_scale, bx, by);
-                if (l < 32 && dst != ~(size_t)0) f.vbuf[dst] = val + f.b2;
+                __syncthreads();
+                for (int it = w; it < 4 * nt; it += FW) {
+                    const int tl = it >> 2, m = it & 3;
+                    const int c = tl * 32 + (l & 31);
+                    const uint4 bx = rs[2 * c], by = rs[2 * c + 1];
+                    vp[(m * FT + tl) * 64 + l] =
+                        mlp_item(wf, T.lut, T.w2s, f.feat_scale, bx, by, tile_kmask(bx, by), m);
+                }
+                __syncthreads();
+                for (int c = t; c < nt * 32; c += 64 * FW) {
+                    const int tl = c >> 5, col = c & 31;
+                    const int r = (tb + tl) * 32 + col;
+                    if (r < nr) {
+                        float vh[2];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int q = tl * 64 + col + 32 * h;
+                            vh[h] = ((vp[q] + vp[FT * 64 + q]) + vp[2 * FT * 64 + q]) + vp[3 * FT * 64 + q];
+                        }
+                        f.vbuf[vslot(r)] = (vh[0] + vh[1]) + f.b2;
+                    }
+                }
             }
+            if (prof) tw[0] += wall_clock64() - m0;
             __syncthreads();
+            tick(3);
             // ---- 4. action choice + env step (the overlay is free again: scratch)
             if (live) {
                 const int n_full = T.cnt[w];
                 const int n = n_full < e.max_legal ? n_full : e.max_legal;
                 if (n <= 0) {
-                    if (l == 0) step_lane_core(e, i, -1, e.rows + (size_t)i * 8, 0.0f, 0.0f, 0);
+                    lane_advance(e, i, st, -1, e.rows + (size_t)i * 8, 0.0f, 0.0f, 0, l == 0);
                 } else {
                     float* x = (float*)lds + (size_t)w * (F_OVL / 4 / FW);
                     const float* vv = f.vbuf + (size_t)i * (f.cap + 1);
                     const float Tm = e.temperature;
+                    const unsigned long long s0 = prof ? wall_clock64() : 0ull;
                     for (int k = l; k < n; k += 64) x[k] = vv[1 + k] / Tm;
                     wave_sync();
-                    const int pick = pick_action(x, n, e.greedy != 0, lane_uniform(e, i));
-                    if (l == 0)
-                        step_lane_core(e, i, pick, f.cand + ((size_t)i * f.cap + pick) * 8, vv[0], vv[1 + pick],
-                                       n_full);
+                    const unsigned long long s1 = prof ? wall_clock64() : 0ull;
+                    const int pick = pick_action(x, n, e.greedy != 0, lane_uniform(e, i, st.ctr));
+                    const unsigned long long s2 = prof ? wall_clock64() : 0ull;
+                    lane_advance(e, i, st, pick, f.cand + ((size_t)i * f.cap + pick) * 8, vv[0], vv[1 + pick],
+                                 n_full, l == 0);
+                    if (prof) {
+                        const unsigned long long s3 = wall_clock64();
+                        tw[1] += s1 - s0;
+                        tw[2] += s2 - s1;
+                        tw[3] += s3 - s2;
+                    }
                 }
             }
             __syncthreads();
+            tick(4);
+            if (prof && t == 0) ph[5] += 1;
+        }
+        if (live && l == 0) lane_store(e, i, st);
+    }
+    if (prof) {
+        unsigned long long* P = f.prof + (size_t)blockIdx.x * 16;
+        if (t == 0)
+            for (int k = 0; k < 6; ++k) atomicAdd(P + k, ph[k]);
+        if (l == 0) {
+            atomicAdd(P + 6, tj);
+            for (int k = 0; k < 4; ++k) atomicAdd(P + 7 + k, tw[k]);
         }
     }
     if (t == 0) {
@@ -219,8 +309,10 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
-        if (hipFuncSetAttribute((const void*)bgx::fused_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                bgx::F_LDS) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)bgx::fused_step_kernel<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS) != hipSuccess ||
+            hipFuncSetAttribute((const void*)bgx::fused_step_kernel<true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS) != hipSuccess)
             return hipErrorInvalidValue;
     }
     if (args->n_steps <= 0 || args->e.L <= 0) return hipSuccess;
@@ -229,6 +321,9 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
     const int groups = (args->e.L + bgx::FW - 1) / bgx::FW;
     int blocks = groups < n_cu ? groups : n_cu;
     if (blocks > args->ws_blocks) blocks = args->ws_blocks;
-    hipLaunchKernelGGL(bgx::fused_step_kernel, dim3(blocks), dim3(64 * bgx::FW), bgx::F_LDS, stream, *args);
+    if (args->prof)
+        hipLaunchKernelGGL(bgx::fused_step_kernel<true>, dim3(blocks), dim3(64 * bgx::FW), bgx::F_LDS, stream, *args);
+    else
+        hipLaunchKernelGGL(bgx::fused_step_kernel<false>, dim3(blocks), dim3(64 * bgx::FW), bgx::F_LDS, stream, *args);
     return hipGetLastError();
 }

@@ -129,6 +129,8 @@ struct FusedArgs {
     int ws_slots;
     size_t ws_words_per_block;
     int force_tier;              // test hook (BGX_MG_TEST_TIER)
+    unsigned long long* prof;    // development (BGX_FUSED_PROF): [gridDim.x][16] phase clocks, or null
+    int exp;                     // development (BGX_FUSED_EXP): variant bits
 };
 
 }  // namespace bgx

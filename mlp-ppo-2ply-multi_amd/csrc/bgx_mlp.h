@@ -60,98 +60,68 @@ BGX_DEV uint4 lut_entry(uint32_t b, float sc) {
     return *(const uint4*)&f;
 }
 
-// One 32-board tile through the MLP on one wavefront (the mlp_kernel<1, NW>
-// sequence: same MFMA order, same epilogue order, so the same bits). bx / by =
-// the packed board of column (lane & 31) (zeros for padding columns); wf / lut
-// / w2s = the LDS-resident W fragments, feature LUT and value-head weights.
-// Returns w2 . sigmoid(W1 x + b1) for the lane's column (both lane halves
-// hold it); the caller adds b2.
-BGX_DEV float mlp_tile_value(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx, uint4 by) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int h = lane >> 5;
-    floatx16 acc[4];
+// Nonzero k-steps of a 32-board tile: k-step s < 12 covers the four point
+// slots in half (s & 1) of packed word s >> 1; a k-step whose slots are empty
+// on every board of the tile has an all-zero B fragment, and the MFMA of a zero
+// fragment adds exact zeros, so skipping it leaves the accumulator's bits
+// unchanged. k-step 12 (bars, borne-off, side to move, bias) always runs.
+BGX_DEV uint32_t tile_kmask(uint4 bx, uint4 by) {
+    const uint32_t wd[6] = {bx.x, bx.y, bx.z, bx.w, by.x, by.y};
+    uint32_t m = 1u << 12;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[m][r] = 0.0f;
-    uint4 ch = wf[((0 * 4 + 0) * KSTEPS + 0) * 64 + lane];
-    uint4 cl = wf[((1 * 4 + 0) * KSTEPS + 0) * 64 + lane];
-    half8 b = feat_frag(bx, by, 0, h, lut, fs);
-#pragma unroll 1
-    for (int s = 0; s < KSTEPS; ++s) {
-        const int sn = s + 1 < KSTEPS ? s + 1 : s;
-        const half8 nb = feat_frag(bx, by, sn, h, lut, fs);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int s2 = m < 3 ? s : sn, m2 = m < 3 ? m + 1 : 0;
-            const uint4 nh = wf[((0 * 4 + m2) * KSTEPS + s2) * 64 + lane];
-            const uint4 nl = wf[((1 * 4 + m2) * KSTEPS + s2) * 64 + lane];
-            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ch, b, acc[m], 0, 0, 0);
-            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&cl, b, acc[m], 0, 0, 0);
-            ch = nh;
-            cl = nl;
-        }
-        b = nb;
+    for (int s = 0; s < 12; ++s) {
+        const uint32_t half = (wd[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
+        m |= ballot(half != 0u) ? 1u << s : 0u;
     }
-    float v = 0.0f;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
-            const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int r = 4 * g + k;
-                const float ex = __builtin_amdgcn_exp2f(acc[m][r]);
-                v = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), v);
-                if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    }
-    return v + __shfl_xor(v, 32, 64);
+    return m;
 }
 
-// mlp_tile_value with one m-tile (32 hidden rows) at a time: 16 accumulator
-// registers instead of 64 (for the fused lane kernel's 128-register budget).
-// The per-(m, column) MFMA chain (k-steps 0..12, hi then lo) and the epilogue
-// order (m, then r) are those of mlp_tile_value, so the result has the same bits.
-BGX_DEV float mlp_tile_value_m(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx, uint4 by) {
+// Epilogue order (every MLP kernel sums V the same way, so a row's V has the
+// same bits whichever kernel, tile or wave computes it): lane half h of column
+// c holds 16 hidden rows of each m-tile; p_m = fma chain over those rows
+// (r = 0..15) from 0, v_h = ((p_0 + p_1) + p_2) + p_3, V = (v_h + v_(1-h)) + b2.
+//
+// One (32-board tile, m-tile) item on one wavefront: the MFMA chain over the
+// tile's nonzero k-steps (tile_kmask; ascending, hi then lo) and the partial
+// p_m of the lane's column half. 16 accumulator registers.
+BGX_DEV float mlp_item(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx, uint4 by,
+                       uint32_t kmask, int m) {
     const int lane = (int)(threadIdx.x & 63);
     const int h = lane >> 5;
-    float v = 0.0f;
-#pragma unroll 1
-    for (int m = 0; m < 4; ++m) {
-        floatx16 acc;
+    floatx16 acc;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-        uint4 ch = wf[((0 * 4 + m) * KSTEPS + 0) * 64 + lane];
-        uint4 cl = wf[((1 * 4 + m) * KSTEPS + 0) * 64 + lane];
-        half8 b = feat_frag(bx, by, 0, h, lut, fs);
-#pragma unroll 1
-        for (int s = 0; s < KSTEPS; ++s) {
-            const int sn = s + 1 < KSTEPS ? s + 1 : s;
-            const uint4 nh = wf[((0 * 4 + m) * KSTEPS + sn) * 64 + lane];
-            const uint4 nl = wf[((1 * 4 + m) * KSTEPS + sn) * 64 + lane];
-            const half8 nb = feat_frag(bx, by, sn, h, lut, fs);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ch, b, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&cl, b, acc, 0, 0, 0);
-            ch = nh;
-            cl = nl;
-            b = nb;
-        }
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    // k-steps fully unrolled, fragments of step s in slot s % 3, loaded two
+    // steps ahead; zero k-steps (uniform mask bits) skip their MFMAs
+    uint4 ah[3], al[3];
+    half8 b[3];
+    auto load = [&](int s) {
+        ah[s % 3] = wf[((0 * 4 + m) * KSTEPS + s) * 64 + lane];
+        al[s % 3] = wf[((1 * 4 + m) * KSTEPS + s) * 64 + lane];
+        b[s % 3] = feat_frag(bx, by, s, h, lut, fs);
+    };
+    load(0);
+    load(1);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
-            const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float ex = __builtin_amdgcn_exp2f(acc[4 * g + k]);
-                v = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), v);
-            }
+    for (int s = 0; s < KSTEPS; ++s) {
+        if (s + 2 < KSTEPS) load(s + 2);
+        if (kmask & (1u << s)) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah[s % 3], b[s % 3], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al[s % 3], b[s % 3], acc, 0, 0, 0);
         }
     }
-    return v + __shfl_xor(v, 32, 64);
+    float p = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
+        const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float ex = __builtin_amdgcn_exp2f(acc[4 * g + k]);
+            p = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), p);
+        }
+    }
+    return p;
 }
 
 }  // namespace bgx

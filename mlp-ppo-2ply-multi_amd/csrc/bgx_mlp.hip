@@ -118,12 +118,14 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
             for (int q = 0; q < NT; ++q) b[q] = nb[q];
         }
         float v[NT];
-#pragma unroll
-        for (int q = 0; q < NT; ++q) v[q] = 0.0f;
         // sigmoid(h) = 1 / (1 + 2^acc) (acc = -h log2 e); w2 of the lane's hidden
-        // rows j0 = 32m + (r & 3) + 8(r >> 2) + 4h from LDS, four at a time
+        // rows j0 = 32m + (r & 3) + 8(r >> 2) + 4h from LDS, four at a time;
+        // summed in the canonical order (bgx_mlp.h, epilogue order)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
+            float pm[NT];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) pm[q] = 0.0f;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
@@ -134,11 +136,13 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
 #pragma unroll
                     for (int q = 0; q < NT; ++q) {
                         const float ex = __builtin_amdgcn_exp2f(acc[m][q][r]);
-                        v[q] = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), v[q]);
+                        pm[q] = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), pm[q]);
                     }
                     if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
                 }
             }
+#pragma unroll
+            for (int q = 0; q < NT; ++q) v[q] = m == 0 ? pm[q] : v[q] + pm[q];
         }
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
             for (int s = 0; s < KSTEPS - 1; ++s) b[s][q] = feat_frag(bx, by, s, h, lut, a.feat_scale);
             w6[q] = by.z;
         }
-        float v[NT] = {0.0f, 0.0f};
+        float v[NT] = {0.0f, 0.0f}, pm[NT] = {0.0f, 0.0f};   // canonical epilogue order (bgx_mlp.h)
         floatx16 acc[2][NT];
         // A pair for (m, s) = (0, 0); each step loads the next pair before its MFMAs
         uint4 ah = wf[((0 * 4 + 0) * KSTEPS + 0) * 64 + lane];
@@ -227,7 +231,14 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
                 // tile m-1's epilogue, spread over k-steps 0..7 (2 rows per step per board tile)
                 if (m > 0 && s < 8) {
 #pragma unroll
-                    for (int q = 0; q < NT; ++q) epi_pair(acc[prv][q], m - 1, 2 * s, h, w2s, v[q]);
+                    for (int q = 0; q < NT; ++q) epi_pair(acc[prv][q], m - 1, 2 * s, h, w2s, pm[q]);
+                    if (s == 7) {
+#pragma unroll
+                        for (int q = 0; q < NT; ++q) {
+                            v[q] = m == 1 ? pm[q] : v[q] + pm[q];
+                            pm[q] = 0.0f;
+                        }
+                    }
                 }
                 ah = nh;
                 al = nl;
@@ -237,7 +248,9 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2)
 #pragma unroll
-            for (int q = 0; q < NT; ++q) epi_pair(acc[1][q], 3, r, h, w2s, v[q]);
+            for (int q = 0; q < NT; ++q) epi_pair(acc[1][q], 3, r, h, w2s, pm[q]);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) v[q] += pm[q];
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             v[q] += __shfl_xor(v[q], 32, 64);

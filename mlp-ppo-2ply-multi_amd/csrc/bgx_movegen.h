@@ -270,6 +270,8 @@ BGX_DEV Node nd_board(const Root& R, uint32_t key) {
 
 // ------------------------------------------------------------------ job I/O
 struct JobIn { Root R; int d0, d1; bool skip; };
+BGX_DEV JobIn make_job(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6,
+                       int player, int d0, int d1);
 
 BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
     JobIn in;
@@ -315,13 +317,24 @@ BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
             in.d1 = a.in_dice[2 * j + 1];
         }
     }
+    const bool skip = in.skip;
+    in = make_job(w0, w1, w2, w3, w4, w5, w6, player, in.d0, in.d1);
+    in.skip = skip;
+    return in;
+}
+
+// job from a packed board's words 0..6, the mover and the dice
+BGX_DEV JobIn make_job(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6,
+                       int player, int d0, int d1) {
+    JobIn in;
+    in.skip = false;
     // the job is wave-uniform: pin its words in SGPRs so the root analysis
     // below (and node_moves on the root) runs on the scalar unit, not VALU
     w0 = uniformu(w0); w1 = uniformu(w1); w2 = uniformu(w2); w3 = uniformu(w3);
     w4 = uniformu(w4); w5 = uniformu(w5); w6 = uniformu(w6);
     player = uniform(player);
-    in.d0 = uniform(in.d0);
-    in.d1 = uniform(in.d1);
+    in.d0 = uniform(d0);
+    in.d1 = uniform(d1);
     const bool p2 = player != 0;
     Root& R = in.R;
     R.m0 = p2 ? w3 : w0; R.m1 = p2 ? w4 : w1; R.m2 = p2 ? w5 : w2;
