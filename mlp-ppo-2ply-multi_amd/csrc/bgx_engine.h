@@ -31,6 +31,33 @@ struct LaneRng {
     }
 };
 
+// The same stream drawn by a whole wavefront (one lane's game): lane k
+// evaluates Philox at counter base + k, so 64 draws cost one Philox
+// evaluation; draws come back by readlane (the counter is wave-uniform).
+struct WaveRng {
+    uint64_t key, ctr, base;
+    u32x4 batch;
+    BGX_DEV void refill() {
+        base = ctr;
+        batch = philox(key, 0x5EED0000ull, base + (uint64_t)lane_id());
+    }
+    BGX_DEV u32x4 at(int k) const {   // counter base + k, k < 64 (wave-uniform)
+        return {(uint32_t)__builtin_amdgcn_readlane((int)batch.x, k), (uint32_t)__builtin_amdgcn_readlane((int)batch.y, k),
+                (uint32_t)__builtin_amdgcn_readlane((int)batch.z, k), (uint32_t)__builtin_amdgcn_readlane((int)batch.w, k)};
+    }
+    BGX_DEV u32x4 next() {
+        if (ctr - base >= 64u) refill();
+        const u32x4 r = at((int)(ctr - base));
+        ++ctr;
+        return r;
+    }
+    BGX_DEV void roll(int& a, int& b) {
+        u32x4 r = next();
+        a = die_from(r.x);
+        b = die_from(r.y);
+    }
+};
+
 // packed initial board (immutable_board.py:27-70): P1 {0:2, 11:5, 16:3, 18:5}, P2 {23:2, 12:5, 7:3, 5:5}
 BGX_DEV void initial_packed(uint32_t* w) {
     w[0] = 0x2u;                       // P1 point 0: 2
@@ -54,7 +81,8 @@ BGX_DEV void store_packed(uint32_t* p, const uint32_t* w) {
 BGX_DEV void set_flag(uint32_t* w, int p) { w[6] = (w[6] & 0xFFFFu) | ((uint32_t)p << 16); }
 
 // reset (backgammon_env.py:92-128); returns starter, leaves first dice in d0/d1
-BGX_DEV int new_game(LaneRng& rng, uint32_t* w, int& d0, int& d1) {
+template <typename Rng>
+BGX_DEV int new_game(Rng& rng, uint32_t* w, int& d0, int& d1) {
     initial_packed(w);
     int a, b;
     do { rng.roll(a, b); } while (a == b);
@@ -153,14 +181,15 @@ BGX_DEV void lane_store(const EngineDev& e, int i, const LaneState& s) {
 // One game lane's env step after its action is chosen (BackgammonEnv.step,
 // backgammon_env.py:130-221, + the worker's Experience, worker.py:101-162):
 // apply, judge, record, and on game end append the episode header and reset.
-// action < 0 (or no legal move): pass. `chosen` = the packed row of candidate
-// `action`, vs / va = V(s) / V(a), n_full = the full candidate count. The
+// action < 0 (or no legal move): pass. `nb` = the packed board (8 words) of
+// candidate `action`, vs / va = V(s) / V(a), n_full = the full candidate count. The
 // state update runs on every calling thread (a wave keeps its lane's state
 // uniform in registers); only `lead` writes memory (record, episode header,
 // the lane's board row).
-BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, int action, const uint32_t* chosen, float vs,
+template <typename Rng>
+BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, Rng& rng, int action, const uint32_t* nb, float vs,
                           float va, int n_full, bool lead) {
-    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), s.ctr};
+    rng.ctr = s.ctr;
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
     bool done = false;
     int win_type = 0, winner = -1;
@@ -172,8 +201,6 @@ BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, int action, c
         s.flags |= 16u << s.p;
         rng.ctr++;   // the sampling uniform (lane_uniform)
         const int a = action;
-        uint32_t nb[8];
-        load_packed(chosen, nb);
         const int mover = s.p;
         const int dd0 = s.d0, dd1 = s.d1;
         const Outcome o = judge(nb, mover, s.flags);
@@ -241,8 +268,10 @@ BGX_DEV void step_lane(const EngineDev& e, int i, int action) {
     const bool act = n > 0 && action >= 0;
     LaneState s;
     lane_load(e, i, s);
-    lane_advance(e, i, s, action, e.rows + (size_t)(base + (act ? action : 0)) * 8, e.V[i],
-                 act ? e.V[base + action] : 0.0f, n_full, true);
+    uint32_t nb[8];
+    load_packed(e.rows + (size_t)(base + (act ? action : 0)) * 8, nb);
+    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), s.ctr};
+    lane_advance(e, i, s, rng, action, nb, e.V[i], act ? e.V[base + action] : 0.0f, n_full, true);
     lane_store(e, i, s);
 }
 
@@ -253,23 +282,26 @@ BGX_DEV float lane_uniform(const EngineDev& e, int i, uint64_t ctr) {
 }
 BGX_DEV float lane_uniform(const EngineDev& e, int i) { return lane_uniform(e, i, e.rng[i]); }
 
-// Action choice over the scores x[0..m) (wave-private LDS, m >= 1) by one
-// wavefront: softmax(x) + inverse-CDF sample at uniform u (worker.py:137-143,
+// Action choice over the scores x(0..m-1) (a functor; m >= 1) by one
+// wavefront: softmax + inverse-CDF sample at uniform u (worker.py:137-143,
 // torch Categorical), or with `greedy` the argmax, first maximum
 // (play_versus_ai.py:188-195; the temperature does not change it).
-BGX_DEV int pick_action(const float* x, int m, bool greedy, float u) {
+template <typename X>
+BGX_DEV int pick_action(X x, int m, bool greedy, float u) {
     const int l = lane_id();
     float mx = -INFINITY;
-    for (int k = l; k < m; k += 64) mx = fmaxf(mx, x[k]);
+    for (int k = l; k < m; k += 64) mx = fmaxf(mx, x(k));
     mx = lane63f(wave_incl_maxf(mx));
     float sum = 0.0f;
-    for (int k = l; k < m; k += 64) sum += __expf(x[k] - mx);
+    for (int k = l; k < m; k += 64) sum += __expf(x(k) - mx);
     sum = lane63f(wave_incl_scanf(sum));
     if (greedy) {
         float bv = -INFINITY;
         int bk = 0x7FFFFFFF;
-        for (int k = l; k < m; k += 64)
-            if (x[k] > bv) { bv = x[k]; bk = k; }
+        for (int k = l; k < m; k += 64) {
+            const float xk = x(k);
+            if (xk > bv) { bv = xk; bk = k; }
+        }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             const float ov = __shfl_xor(bv, off, 64);
@@ -283,7 +315,7 @@ BGX_DEV int pick_action(const float* x, int m, bool greedy, float u) {
     float carry = 0.0f;
     for (int b = 0; b < m; b += 64) {
         const int k = b + l;
-        const float p = wave_incl_scanf(k < m ? __expf(x[k] - mx) : 0.0f);   // inclusive scan over the wave
+        const float p = wave_incl_scanf(k < m ? __expf(x(k) - mx) : 0.0f);   // inclusive scan over the wave
         const uint64_t hit = ballot(k < m && t < carry + p);
         if (hit) {
             pick = b + __ffsll((unsigned long long)hit) - 1;

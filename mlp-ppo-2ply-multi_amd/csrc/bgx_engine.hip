@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
         x[k] = v;
     }
     wave_sync();
-    const int pick = pick_action(x, m, e.greedy != 0, lane_uniform(e, i));
+    const int pick = pick_action([&](int k) { return x[k]; }, m, e.greedy != 0, lane_uniform(e, i));
     if (l == 0) step_lane(e, i, k4 ? e.sel[4 * i + pick] - base : pick);
 }
 
