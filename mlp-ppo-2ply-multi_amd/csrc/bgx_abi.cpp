@@ -152,10 +152,12 @@ struct bgx_engine {
     float* fvbuf = nullptr;
     int fcap = 0;
     unsigned long long* fprof = nullptr;   // BGX_FUSED_PROF: phase clocks, printed at destroy
-    // harvest
+    // harvest: records of at most L x ring (every unharvested record of every lane)
     uint32_t* out_records = nullptr;
-    int out_cap = 0;
-    int32_t* d_offs = nullptr;
+    int32_t* d_offs = nullptr;     // [ep_cap + 1]
+    uint32_t* d_info = nullptr;    // [4] harvest_scan_kernel totals
+    uint32_t* h_info = nullptr;    // pinned host copy
+    hipEvent_t hev = nullptr;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;   // pairs: movegen, mlp
@@ -427,11 +429,13 @@ int bgx_engine_destroy(bgx_engine* e) {
     }
     void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
                   e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
-                  e->d_offs, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
+                  e->d_offs, e->d_info, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
                   e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
     for (void* p : ps) hipFree(p);
     for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
     if (e->gexec) hipGraphExecDestroy(e->gexec);
+    if (e->hev) hipEventDestroy(e->hev);
+    if (e->h_info) hipHostFree(e->h_info);
     if (e->cap) hipStreamDestroy(e->cap);
     bgx_net_destroy(e->net);
     delete e;
@@ -475,6 +479,11 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     ALLOC(d.harv, L);
     ALLOC(d.ring, (size_t)L * cfg->ring * bgx::REC_WORDS);
     ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
+    ALLOC(e->out_records, (size_t)L * cfg->ring * bgx::REC_WORDS);
+    ALLOC(e->d_offs, (size_t)ep_cap + 1);
+    ALLOC(e->d_info, 4);
+    if (!rc && hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        rc = fail(BGX_E_HIP, "hipHostMalloc failed");
     e->ovf_cap = 1 << 16;
     e->ws_waves = 256;   // one global-memory fallback slice per tier-2 block
     e->ws_slots = 16384;
@@ -777,36 +786,25 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
     if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest: null pointer");
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipStreamSynchronize(e->last));
-    HIP_TRY(hipStreamSynchronize(s));
-    int rc = check_flags(e);
-    if (rc) return rc;
-    unsigned n_eps = 0;
-    HIP_TRY(hipMemcpy(&n_eps, e->ctr + C_EP, 4, hipMemcpyDeviceToHost));
-    if ((int)n_eps > e->d.ep_cap) n_eps = (unsigned)e->d.ep_cap;
-    std::vector<uint32_t> hdr((size_t)n_eps * bgx::EP_WORDS);
-    if (n_eps) HIP_TRY(hipMemcpy(hdr.data(), e->d.ep_list, hdr.size() * 4, hipMemcpyDeviceToHost));
-    std::vector<int32_t> offs(n_eps + 1, 0);
-    for (unsigned i = 0; i < n_eps; ++i) offs[i + 1] = offs[i] + (int32_t)hdr[(size_t)i * bgx::EP_WORDS + 3];
-    const int total = offs[n_eps];
-    if (total > e->out_cap) {
-        hipFree(e->out_records);
-        e->out_records = nullptr;
-        const int cap = total + total / 2 + 1024;
-        if (dalloc(&e->out_records, (size_t)cap * bgx::REC_WORDS)) return BGX_E_HIP;
-        e->out_cap = cap;
+    // order after the engine's last step (another stream): an event, no host wait
+    if (e->last != s) {
+        if (!e->hev) HIP_TRY(hipEventCreateWithFlags(&e->hev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e->hev, e->last));
+        HIP_TRY(hipStreamWaitEvent(s, e->hev, 0));
     }
-    if ((int)offs.size() > 0) {
-        hipFree(e->d_offs);
-        e->d_offs = nullptr;
-        if (dalloc(&e->d_offs, offs.size())) return BGX_E_HIP;
-        HIP_TRY(hipMemcpy(e->d_offs, offs.data(), offs.size() * 4, hipMemcpyHostToDevice));
-    }
-    HIP_TRY(bgx_launch_gather(&e->d, e->d.ep_list, e->d_offs, (int)n_eps, e->out_records, s));
+    // offsets and totals on the device (harvest_scan_kernel), gather, then ONE
+    // small copy of {episodes, records, error flags} to the host
+    HIP_TRY(bgx_launch_harvest(&e->d, e->d_offs, e->d_info, e->out_records, s));
+    HIP_TRY(hipMemcpyAsync(e->h_info, e->d_info, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(hipMemset(e->ctr + C_EP, 0, 4));
-    out->n_episodes = (int)n_eps;
-    out->n_records = total;
+    const uint32_t flags = e->h_info[2];
+    if (flags) {
+        HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
+        return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
+                    "workspace, 8 experience ring, 16 episode list)", flags);
+    }
+    out->n_episodes = (int)e->h_info[0];
+    out->n_records = (int)e->h_info[1];
     out->d_headers = e->d.ep_list;
     out->d_records = e->out_records;
     return BGX_OK;

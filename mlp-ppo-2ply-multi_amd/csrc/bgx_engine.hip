@@ -215,21 +215,62 @@ __global__ __launch_bounds__(256) void two_ply_reduce_kernel(const float* __rest
 }
 
 // harvest: copy finished episodes' records out of the lane rings
-__global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
-                                                     const int32_t* __restrict__ offs, int n_eps,
-                                                     uint32_t* __restrict__ out) {
-    const int ep = blockIdx.x;
-    if (ep >= n_eps) return;
-    const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
-    const int lane = (int)h[0] - e.lane_base;
-    const uint32_t first = h[2], nrec = h[3];
-    const size_t words = (size_t)nrec * REC_WORDS;
-    for (size_t q = threadIdx.x; q < words; q += blockDim.x) {
-        const uint32_t r = (uint32_t)(q / REC_WORDS), k = (uint32_t)(q % REC_WORDS);
-        const uint32_t slot = (first + r) % (uint32_t)e.R;
-        out[((size_t)offs[ep] + r) * REC_WORDS + k] = e.ring[((size_t)lane * e.R + slot) * REC_WORDS + k];
+// harvest, step 1 (one workgroup): record offsets of the finished episodes
+// (exclusive scan of their record counts) and the harvest totals, read on the
+// device so the host needs one small copy: info = {episodes, records, error
+// flags, episodes appended (incl. any past ep_cap)}; the episode list restarts.
+__global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t* __restrict__ offs,
+                                                            uint32_t* __restrict__ info) {
+    __shared__ int wsum[16];
+    const unsigned n_raw = *e.ep_count;
+    const int n = (int)n_raw < e.ep_cap ? (int)n_raw : e.ep_cap;
+    const int t = (int)threadIdx.x, w = t >> 6;
+    int carry = 0;
+    for (int b = 0; b < n; b += 1024) {
+        const int k = b + t;
+        const int c = k < n ? (int)e.ep_list[(size_t)k * EP_WORDS + 3] : 0;
+        const int incl = wave_incl_scan(c);
+        if (lane_id() == 63) wsum[w] = incl;
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int x = wsum[q];
+            before += q < w ? x : 0;
+            total += x;
+        }
+        if (k < n) offs[k] = carry + before + incl - c;
+        carry += total;
+        __syncthreads();
     }
-    if (threadIdx.x == 0) atomicMax(e.harv + lane, first + nrec);
+    if (t == 0) {
+        offs[n] = carry;
+        info[0] = (uint32_t)n;
+        info[1] = (uint32_t)carry;
+        info[2] = *e.err_flags;
+        info[3] = n_raw;
+        *e.ep_count = 0u;
+    }
+}
+
+// harvest, step 2: copy finished episodes' records out of the lane rings
+// (persistent grid; the episode count comes from harvest_scan_kernel)
+__global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
+                                                     const int32_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ info, uint32_t* __restrict__ out) {
+    const int n_eps = (int)info[0];
+    for (int ep = blockIdx.x; ep < n_eps; ep += gridDim.x) {
+        const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
+        const int lane = (int)h[0] - e.lane_base;
+        const uint32_t first = h[2], nrec = h[3];
+        const size_t words = (size_t)nrec * REC_WORDS;
+        for (size_t q = threadIdx.x; q < words; q += blockDim.x) {
+            const uint32_t r = (uint32_t)(q / REC_WORDS), k = (uint32_t)(q % REC_WORDS);
+            const uint32_t slot = (first + r) % (uint32_t)e.R;
+            out[((size_t)offs[ep] + r) * REC_WORDS + k] = e.ring[((size_t)lane * e.R + slot) * REC_WORDS + k];
+        }
+        if (threadIdx.x == 0) atomicMax(e.harv + lane, first + nrec);
+    }
 }
 
 }  // namespace bgx
@@ -264,11 +305,11 @@ extern "C" hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, dou
                        out);
     return hipGetLastError();
 }
-extern "C" hipError_t bgx_launch_gather(const bgx::EngineDev* e, const uint32_t* headers,
-                                        const int32_t* offsets, int n_eps, uint32_t* out,
-                                        hipStream_t stream) {
-    if (n_eps <= 0) return hipSuccess;
-    hipLaunchKernelGGL(bgx::gather_kernel, dim3(n_eps), dim3(256), 0, stream, *e, headers, offsets, n_eps,
-                       out);
+extern "C" hipError_t bgx_launch_harvest(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info,
+                                         uint32_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::harvest_scan_kernel, dim3(1), dim3(1024), 0, stream, *e, offsets, info);
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(bgx::gather_kernel, dim3(1024), dim3(256), 0, stream, *e, e->ep_list, offsets, info, out);
     return hipGetLastError();
 }

@@ -153,6 +153,6 @@ hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t
                            const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
                            hipStream_t stream);
 hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out, hipStream_t stream);
-hipError_t bgx_launch_gather(const bgx::EngineDev* e, const uint32_t* headers, const int32_t* offsets,
-                             int n_eps, uint32_t* out, hipStream_t stream);
+hipError_t bgx_launch_harvest(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* out,
+                              hipStream_t stream);
 }
