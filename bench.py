@@ -230,7 +230,8 @@ def main():
     ap.add_argument("--ply", type=int, default=1)
     ap.add_argument("--k-top", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--harvest-every", type=int, default=100)
+    ap.add_argument("--harvest-every", type=int, default=300,
+                    help="steps per bgx_step launch between harvests (<= ring - max_steps = 340)")
     ap.add_argument("--two-ply-steps", type=int, default=100, help="extra 2-ply (K=4) measurement; 0 = skip")
     ap.add_argument("--kall-steps", type=int, default=20,
                     help="extra 2-ply K=all measurement (configs[2]: ~21 x C reply boards per decision); 0 = skip")

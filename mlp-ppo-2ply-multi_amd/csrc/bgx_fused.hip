@@ -110,21 +110,24 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
                 M.S = S_T1;
                 M.map[l] = 0u;
                 wave_sync();
+                // doubles (the long jobs) first, dealt out snake-wise: wave w takes
+                // positions w and 2 NW - 1 - w of that order (static, no atomics)
+                const bool dbl = l < nlive && T.st[l].d0 == T.st[l].d1;
+                const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(l < nlive && !dbl);
+                const int nd = __popc(dmask);
                 for (int q = 0; q < LPW; ++q) {
-                    const int v = w * LPW + q;
-                    int nf = 0;
-                    if (v < nlive) {
-                        const LaneState& st = T.st[v];
-                        if (l < 8)
-                            T.job[v][l] =
-                                l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
-                        const JobIn in = make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6],
-                                                  st.p, st.d0, st.d1);
-                        uint32_t* fin = nullptr;
-                        nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, 0x7FFFFFFF);
-                        if (nf >= 0) emit_records<false>(a, g * FL + v, in, fin, nf, 0);
-                        wave_sync();
-                    }
+                    const int k = (q & 1) ? (q + 1) * NW - 1 - w : q * NW + w;
+                    if (k >= nlive) continue;
+                    const int v = k < nd ? select_bit(dmask, k) : select_bit(omask, k - nd);
+                    const LaneState& st = T.st[v];
+                    if (l < 8)
+                        T.job[v][l] = l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
+                    const JobIn in =
+                        make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6], st.p, st.d0, st.d1);
+                    uint32_t* fin = nullptr;
+                    const int nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, 0x7FFFFFFF);
+                    if (nf >= 0) emit_records<false>(a, g * FL + v, in, fin, nf, 0);
+                    wave_sync();
                     if (l == 0) T.cnt[v] = nf;
                 }
                 if (prof) tj += wall_clock64() - j0;
