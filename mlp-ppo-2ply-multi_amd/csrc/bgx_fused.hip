@@ -238,12 +238,24 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
             const unsigned long long m0 = prof ? wall_clock64() : 0ull;
             for (int tb = 0; tb < n_tiles; tb += FT) {
                 const int nt = n_tiles - tb < FT ? n_tiles - tb : FT;
-                for (int it = w; it < 4 * nt; it += NW) {
-                    const int tl = it >> 2, m = it & 3;
-                    const int c = tl * 32 + (l & 31);
-                    const uint4 bx = rs[2 * c], by = rs[2 * c + 1];
-                    vp[(m * FT + tl) * 64 + l] =
-                        mlp_item(wf, T.lut, T.w2s, f.feat_scale, bx, by, tile_kmask(bx, by), m);
+                // items: (tile pair, m-tile); an odd last tile runs alone
+                const int npair = (nt + 1) >> 1;
+                for (int it = w; it < 4 * npair; it += NW) {
+                    const int tp = it >> 2, m = it & 3;
+                    const int t0 = 2 * tp, c0 = t0 * 32 + (l & 31);
+                    const uint4 bx0 = rs[2 * c0], by0 = rs[2 * c0 + 1];
+                    if (t0 + 1 < nt) {
+                        const int c1 = c0 + 32;
+                        const uint4 bx1 = rs[2 * c1], by1 = rs[2 * c1 + 1];
+                        float p0, p1;
+                        mlp_item2(wf, T.lut, T.w2s, f.feat_scale, bx0, by0, bx1, by1,
+                                  tile_kmask(bx0, by0) | tile_kmask(bx1, by1), m, p0, p1);
+                        vp[(m * FT + t0) * 64 + l] = p0;
+                        vp[(m * FT + t0 + 1) * 64 + l] = p1;
+                    } else {
+                        vp[(m * FT + t0) * 64 + l] =
+                            mlp_item(wf, T.lut, T.w2s, f.feat_scale, bx0, by0, tile_kmask(bx0, by0), m);
+                    }
                 }
                 __syncthreads();
                 for (int c = t; c < nt * 32; c += NT) {

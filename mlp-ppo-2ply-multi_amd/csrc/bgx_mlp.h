@@ -124,4 +124,54 @@ BGX_DEV float mlp_item(const uint4* wf, const uint4* lut, const float* w2s, floa
     return p;
 }
 
+// mlp_item over two 32-board tiles at once (same m-tile): each A fragment
+// read from LDS feeds both tiles' MFMAs. kmask = the union of the two tiles'
+// masks (a k-step that is zero for one tile adds exact zeros to it). p0 / p1
+// are the partials of the lane's column in tile 0 / 1.
+BGX_DEV void mlp_item2(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx0, uint4 by0,
+                       uint4 bx1, uint4 by1, uint32_t kmask, int m, float& p0, float& p1) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int h = lane >> 5;
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        acc0[r] = 0.0f;
+        acc1[r] = 0.0f;
+    }
+    uint4 ah[3], al[3];
+    half8 b0[3], b1[3];
+    auto load = [&](int s) {
+        ah[s % 3] = wf[((0 * 4 + m) * KSTEPS + s) * 64 + lane];
+        al[s % 3] = wf[((1 * 4 + m) * KSTEPS + s) * 64 + lane];
+        b0[s % 3] = feat_frag(bx0, by0, s, h, lut, fs);
+        b1[s % 3] = feat_frag(bx1, by1, s, h, lut, fs);
+    };
+    load(0);
+    load(1);
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        if (s + 2 < KSTEPS) load(s + 2);
+        if (kmask & (1u << s)) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah[s % 3], b0[s % 3], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah[s % 3], b1[s % 3], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al[s % 3], b0[s % 3], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al[s % 3], b1[s % 3], acc1, 0, 0, 0);
+        }
+    }
+    float q0 = 0.0f, q1 = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
+        const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float e0 = __builtin_amdgcn_exp2f(acc0[4 * g + k]), e1 = __builtin_amdgcn_exp2f(acc1[4 * g + k]);
+            q0 = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + e0), q0);
+            q1 = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + e1), q1);
+        }
+    }
+    p0 = q0;
+    p1 = q1;
+}
+
 }  // namespace bgx
