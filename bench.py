@@ -177,7 +177,9 @@ def roofline_fused(d, tm):
     if os.path.exists(prof):
         try:
             with open(prof) as f:
-                r["traffic"] = json.load(f).get("1ply_fused", {}).get("fused", {}).get("hbm_bytes_per_launch")
+                per_step = json.load(f).get("1ply_fused", {}).get("fused", {}).get("hbm_bytes_per_step")
+                # PMC bytes per step (tools/profile_round.sh) x the steps of this bench's launches
+                r["traffic"] = per_step * k["steps_per_launch"] if per_step else None
         except Exception:
             r["traffic"] = None
     return r, {"fused_step": k, "fused_step_mfma": m}

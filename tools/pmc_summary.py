@@ -4,7 +4,10 @@ per-launch HBM bytes per leg and kernel group, with the gfx950 correction of
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE reads 1/2 of wide coalesced
 streaming reads, so hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 A bench "movegen launch" is tier 1 + tier 2 (movegen_few/lds + movegen_block);
-the 2-ply leg has two movegen launches and two MLP launches per step."""
+the 2-ply leg has two movegen launches and two MLP launches per step. The
+fused 1-ply leg is one bgx::fused_step_kernel dispatch per 300 steps; its
+bytes are also given per step (bench.py scales them to its own launches)."""
+FUSED_STEPS_PER_DISPATCH = 300
 import collections
 import csv
 import glob
@@ -26,17 +29,22 @@ def per_kernel(path):
 
 
 def group(name):
+    if "fused_step" in name:
+        return "fused"
     return "mlp" if "mlp_kernel" in name else "movegen"
 
 
 def main(out):
     res = {"source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
-                     "--kernel-include-regex 'movegen|mlp_kernel', bench.py 1-ply leg (200 steps) and 2-ply leg (60 steps)",
+                     "fused 1-ply leg (--kernel-include-regex fused_step, 300 steps per dispatch) and 2-ply K=4 leg "
+                     "(--kernel-include-regex 'movegen|mlp_kernel', 60 steps)",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts 1/2 of wide "
                          "coalesced reads; narrow movegen reads are uncalibrated, the raw value is kept beside it)"}
-    for leg in ("1", "2"):
+    for leg in ("1ply_fused", "2ply"):
         f = per_kernel(os.path.join(out, f"pmc_{leg}_FETCH_SIZE"))
         w = per_kernel(os.path.join(out, f"pmc_{leg}_WRITE_SIZE"))
+        if not f and not w:
+            continue
         legd = {"kernels": {}}
         for name in sorted(set(f) | set(w)):
             fk, nf = f.get(name, (0.0, 0))
@@ -44,7 +52,7 @@ def main(out):
             n = max(nf, nw, 1)
             legd["kernels"][name] = {"dispatches": n, "fetch_size_kb_per_dispatch": fk / max(nf, 1),
                                      "write_size_kb_per_dispatch": wk / max(nw, 1)}
-        for g in ("movegen", "mlp"):
+        for g in ("movegen", "mlp", "fused"):
             names = [k for k in legd["kernels"] if group(k) == g]
             if not names:
                 continue
@@ -52,6 +60,8 @@ def main(out):
             # MLP call is one mlp_kernel dispatch
             if g == "movegen":
                 n_launch = sum(legd["kernels"][k]["dispatches"] for k in names if "movegen_block" in k)
+            elif g == "fused":
+                n_launch = sum(legd["kernels"][k]["dispatches"] for k in names)
             else:
                 n_launch = sum(legd["kernels"][k]["dispatches"] for k in names)
             fk = sum(legd["kernels"][k]["fetch_size_kb_per_dispatch"] * legd["kernels"][k]["dispatches"] for k in names)
@@ -59,7 +69,10 @@ def main(out):
             legd[g] = {"kernels": names, "launches": n_launch,
                        "hbm_bytes_per_launch": (2 * fk + wk) * 1024 / n_launch,
                        "hbm_bytes_per_launch_uncorrected": (fk + wk) * 1024 / n_launch}
-        res[f"{leg}ply"] = legd
+            if g == "fused":
+                legd[g]["steps_per_launch"] = FUSED_STEPS_PER_DISPATCH
+                legd[g]["hbm_bytes_per_step"] = legd[g]["hbm_bytes_per_launch"] / FUSED_STEPS_PER_DISPATCH
+        res[leg] = legd
     print(json.dumps(res, indent=1))
 
 
