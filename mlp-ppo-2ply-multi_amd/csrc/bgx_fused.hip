@@ -32,10 +32,17 @@
 namespace bgx {
 
 constexpr int FL = 16;                                   // lanes per workgroup
-constexpr int F_OVL = 16 * Slice<S_T1>::bytes;           // overlay: slices | CoopLds | W + partials + rows
-static_assert(sizeof(CoopLds) <= (size_t)F_OVL, "cooperative tier fits the overlay");
-static_assert(NFRAG * 16 <= F_OVL, "W fragments fit the overlay");
-static_assert(Slice<S_T2>::bytes <= F_OVL, "32 KB slice fits the overlay");
+constexpr int NW = 8;                                    // waves per workgroup (two lanes each, 256 registers)
+// LDS: [scratch | W fragments (resident for the launch) | tail | lane values]
+//  scratch = 8 tier-1 slices (256-slot table, 416-entry frontiers) during
+//  movegen, the 32 KB tier-2 slice, then the MLP partials + staged rows
+constexpr int S1 = 256, F1 = 416;
+constexpr int SL1 = S1 * 8 + 2 * F1 * 4 + 64 * 4;        // 5,632 B
+constexpr int F_SCR = NW * SL1;
+constexpr int F_W = F_SCR;
+constexpr int F_TAIL = F_W + NFRAG * 16;
+static_assert(Slice<S_T2>::bytes <= F_SCR, "32 KB slice fits the scratch");
+constexpr int FT = F_SCR / (4 * 64 * 4 + 32 * 32);        // MLP tiles per batch: partials + staged rows
 
 struct FusedTail {
     uint4 lut[256];                 // feature LUT (bgx_mlp.h lut_entry)
@@ -45,23 +52,24 @@ struct FusedTail {
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
 };
-constexpr int XS = 384;             // V(s), V(candidates 0..XS-2) of each lane kept in LDS (rest: vbuf)
-constexpr int F_LDS = F_OVL + (int)sizeof(FusedTail) + FL * XS * 4;
-constexpr int FT = (F_OVL - NFRAG * 16) / (4 * 64 * 4 + 32 * 32);   // MLP tiles per batch: partials + rows after W
-static_assert(FT >= 4, "partials fit behind W");
+constexpr int XS = 88;              // V(s), V(candidates 0..XS-2) of each lane kept in LDS (rest: vbuf)
+constexpr int F_LDS = F_TAIL + (int)sizeof(FusedTail) + FL * XS * 4;
+static_assert(F_LDS <= 160 * 1024, "fits the CU's LDS");
 
-template <bool PROF, int NW>
+template <bool PROF>
 __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
     constexpr int NT = 64 * NW;          // threads
     constexpr int LPW = FL / NW;         // lanes per wave
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     uint8_t* lds = (uint8_t*)smem;
-    FusedTail& T = *(FusedTail*)(lds + F_OVL);
-    float* xs = (float*)(lds + F_OVL + sizeof(FusedTail));   // [FL][XS] lane values
+    FusedTail& T = *(FusedTail*)(lds + F_TAIL);
+    float* xs = (float*)(lds + F_TAIL + sizeof(FusedTail));   // [FL][XS] lane values
     const EngineDev& e = f.e;
     const int t = (int)threadIdx.x, w = t >> 6, l = lane_id();
     for (int i = t; i < 256; i += NT) T.lut[i] = lut_entry((uint32_t)i, f.feat_scale);
     for (int i = t; i < 128; i += NT) T.w2s[i] = f.rowc[i];
+    uint4* wf = (uint4*)(lds + F_W);   // split-fp16 W fragments, loaded once
+    for (int k = t; k < NFRAG; k += NT) wf[k] = f.wfrag[k];
 
     MovegenArgs a{};
     a.out_mode = OUT_PACKED_SLOT;
@@ -86,9 +94,8 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
             tc = c;
         }
     };
-    uint4* wf = (uint4*)lds;                                    // W fragments (phases 2-3)
-    float* vp = (float*)(lds + NFRAG * 16);                     // [4][FT][64] MLP partials
-    uint4* rs = (uint4*)(lds + NFRAG * 16 + 4 * FT * 64 * 4);   // [FT * 32][2] staged rows
+    float* vp = (float*)lds;                           // [4][FT][64] MLP partials (scratch)
+    uint4* rs = (uint4*)(lds + 4 * FT * 64 * 4);       // [FT * 32][2] staged rows (scratch)
     const int groups = (e.L + FL - 1) / FL;
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int nlive = e.L - g * FL < FL ? e.L - g * FL : FL;
@@ -100,14 +107,14 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
             if (prof && t == 0) tc = wall_clock64();
             {
                 const unsigned long long j0 = prof ? wall_clock64() : 0ull;
-                unsigned long long* sl = smem + (size_t)w * (Slice<S_T1>::bytes / 8);
+                unsigned long long* sl = (unsigned long long*)(lds + (size_t)w * SL1);
                 Mem M;
                 M.tab = sl;
-                M.F = Slice<S_T1>::F;
-                M.fa = (uint32_t*)(sl + S_T1);
-                M.fb = M.fa + M.F;
-                M.map = M.fb + M.F;
-                M.S = S_T1;
+                M.F = F1;
+                M.fa = (uint32_t*)(sl + S1);
+                M.fb = M.fa + F1;
+                M.map = M.fb + F1;
+                M.S = S1;
                 M.map[l] = 0u;
                 wave_sync();
                 // doubles (the long jobs) first, dealt out snake-wise: wave w takes
@@ -164,30 +171,11 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
                     if (r < 0 && l == 0) atomicOr(e.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
                     return r < 0 ? 0 : r;
                 };
-                if (NW != 16 || in.d0 != in.d1 || f.force_tier >= 3) {
-                    if (w == 0) {
-                        const Mem M2 = lds_mem<S_T2>(smem);
-                        int r = f.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M2, fc);
-                        if (r < 0) r = run_global();
-                        if (l == 0) T.cnt[v] = r;
-                    }
-                } else if constexpr (NW == 16) {
-                    CoopLds& C = *(CoopLds*)smem;
-                    uint32_t* fin = nullptr;
-                    const int nfin = coop_doubles(in, C, fin);   // block-uniform
-                    if (nfin >= 0) {
-                        for (int k = t; k < nfin && k < f.cap; k += NT) {
-                            const uint32_t x = fin[k];
-                            emit_one(a, j, in.R,
-                                     (x & PATHF) ? path_board(in.R, x & KEYMASK, in.d0)
-                                                 : rebuild(in.R, x & KEYMASK, in.d0),
-                                     k, 0);
-                        }
-                        if (t == 0) T.cnt[v] = nfin;
-                    } else if (w == 0) {
-                        const int r = run_global();
-                        if (l == 0) T.cnt[v] = r;
-                    }
+                if (w == 0) {   // tier 2: a 32 KB slice in wave 0, then tier 3
+                    const Mem M2 = lds_mem<S_T2>(smem);
+                    int r = f.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M2, fc);
+                    if (r < 0) r = run_global();
+                    if (l == 0) T.cnt[v] = r;
                 }
                 __syncthreads();
                 if (prof) t2c += wall_clock64() - c2;
@@ -227,9 +215,8 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
                     rs[2 * c + 1] = by;
                 }
             };
-            // ---- 3. W fragments into the overlay + the first batch's rows
+            // ---- 3. the first batch's rows into the scratch
             const int n_tiles = (nr + 31) >> 5;
-            for (int k = t; k < NFRAG; k += NT) wf[k] = f.wfrag[k];
             stage(0, n_tiles < FT ? n_tiles : FT);
             __syncthreads();
             tick(2);
@@ -355,21 +342,17 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
 
 }  // namespace bgx
 
-// BGX_FUSED_WAVES=16: one lane per wave (128 registers); default 8 (two lanes per wave, 256 registers)
 extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t stream) {
-    static int n_cu = 0, nw = 8;
+    static int n_cu = 0;
     if (!n_cu) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
-        const void* ks[] = {(const void*)bgx::fused_step_kernel<false, 8>, (const void*)bgx::fused_step_kernel<true, 8>,
-                            (const void*)bgx::fused_step_kernel<false, 16>,
-                            (const void*)bgx::fused_step_kernel<true, 16>};
+        const void* ks[] = {(const void*)bgx::fused_step_kernel<false>, (const void*)bgx::fused_step_kernel<true>};
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS) != hipSuccess)
                 return hipErrorInvalidValue;
-        if (const char* v = getenv("BGX_FUSED_WAVES")) nw = atoi(v) == 16 ? 16 : 8;
     }
     if (args->n_steps <= 0 || args->e.L <= 0) return hipSuccess;
     if (args->cap < 1 || args->cap > 2048) return hipErrorInvalidValue;
@@ -377,17 +360,9 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
     const int groups = (args->e.L + bgx::FL - 1) / bgx::FL;
     int blocks = groups < n_cu ? groups : n_cu;
     if (blocks > args->ws_blocks) blocks = args->ws_blocks;
-    const size_t lds = bgx::F_LDS;
-    if (nw == 16) {
-        if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 16>), dim3(blocks), dim3(1024), lds, stream, *args);
-        else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 16>), dim3(blocks), dim3(1024), lds, stream, *args);
-    } else {
-        if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 8>), dim3(blocks), dim3(512), lds, stream, *args);
-        else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 8>), dim3(blocks), dim3(512), lds, stream, *args);
-    }
+    if (args->prof)
+        hipLaunchKernelGGL(bgx::fused_step_kernel<true>, dim3(blocks), dim3(64 * bgx::NW), bgx::F_LDS, stream, *args);
+    else
+        hipLaunchKernelGGL(bgx::fused_step_kernel<false>, dim3(blocks), dim3(64 * bgx::NW), bgx::F_LDS, stream, *args);
     return hipGetLastError();
 }
