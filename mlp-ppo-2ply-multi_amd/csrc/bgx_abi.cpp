@@ -136,6 +136,7 @@ struct bgx_engine {
     unsigned* ctr = nullptr;   // [3] ep, [4] err; per-step (zeroed each step): [8] flat, [9] reply, [10] ovf, [11] ovf2
     unsigned long long* stats = nullptr;
     int32_t* sel = nullptr;
+    uint32_t* sel_rows = nullptr;
     uint32_t* reply_rows = nullptr;
     float* reply_V = nullptr;
     int32_t* job_off = nullptr;
@@ -427,7 +428,7 @@ int bgx_engine_destroy(bgx_engine* e) {
         }
         hipFree(e->fprof);
     }
-    void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->reply_rows,
+    void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
                   e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
                   e->d_offs, e->d_info, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
                   e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
@@ -507,6 +508,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         // + the slack of one partly used 512-row reservation per resident movegen wave (<= 32 / CU)
         e->reply_cap = L * per_lane + n_cu * 32 * 512;
         ALLOC(e->sel, 4 * L);
+        ALLOC(e->sel_rows, (size_t)4 * L * 8);
         ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
         ALLOC(e->reply_V, e->reply_cap);
         ALLOC(e->job_off, e->jobs_cap);
@@ -542,6 +544,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     d.cand_cnt = e->cand_cnt;
     d.V = e->V;
     d.sel = e->sel;
+    d.sel_rows = e->sel_rows;
     d.job_val = e->job_val;
     d.flat_count = e->ctr + C_FLAT;
     d.reply_count = e->ctr + C_REPLY;
@@ -646,7 +649,9 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             if (e->cfg.k_top == 4) {
                 HIP_TRY(bgx_launch_topk(&e->d, s));
                 b.n_jobs = L * 4 * 21;
-                b.in_rows = e->sel;
+                b.in_packed = e->sel_rows;   // the top-k kernel's copies of the chosen rows
+                b.in_rows = nullptr;
+                b.in_row_base = 0;
             } else {
                 b.n_jobs = 0;
                 b.n_jobs_dev = e->ctr + C_FLAT;

@@ -118,7 +118,12 @@ __global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
     const int base = e.L + e.cand_off[i];
     if (n < 4) {
-        if (l < 4) e.sel[4 * i + l] = -1;
+        if (l < 4) {
+            e.sel[4 * i + l] = -1;
+            uint4* d = (uint4*)(e.sel_rows + (size_t)(4 * i + l) * 8);
+            d[0] = make_uint4(0u, 0u, 0u, 0u);
+            d[1] = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);   // SKIP_ROW (bgx_movegen.h)
+        }
         return;
     }
     float bv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -151,7 +156,14 @@ __global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
             bi[0] = bi[1]; bi[1] = bi[2]; bi[2] = bi[3]; bi[3] = 0x7FFFFFFF;
         }
     }
-    if (l < 4) e.sel[4 * i + l] = base + out;
+    if (l < 4) {
+        // the reply launch reads the chosen boards contiguously (no row indirection)
+        e.sel[4 * i + l] = base + out;
+        const uint4* s = (const uint4*)(e.rows + (size_t)(base + out) * 8);
+        uint4* d = (uint4*)(e.sel_rows + (size_t)(4 * i + l) * 8);
+        d[0] = s[0];
+        d[1] = s[1];
+    }
 }
 
 // 2-ply: per (candidate, roll) job, mean of the top-5 reply values

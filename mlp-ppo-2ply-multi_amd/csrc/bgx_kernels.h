@@ -102,6 +102,7 @@ struct EngineDev {
     const int32_t* cand_cnt;     // [L] full candidate count
     const float* V;              // [L + cand rows] values
     int32_t* sel;                // [L * 4] 2-ply: candidate rows chosen by 1-ply V (or -1)
+    uint32_t* sel_rows;          // [L * 4][8] 2-ply: those rows' packed boards (word 7 = SKIP_ROW: none)
     const float* job_val;        // [L * 4 * 21] 2-ply: top-5 mean per (candidate, roll)
     unsigned* flat_count;        // candidate rows this step (device; zeroed by the step kernel)
     unsigned* reply_count;       // 2-ply reply rows this step (device; zeroed by the step kernel)

@@ -158,20 +158,48 @@ BGX_DEV bool doubles_by_path(const Root& R) {
     const uint32_t home = R.player == 0 ? nibsum(R.m2 >> 8) : nibsum(R.m0 & 0xFFFFFFu);
     return 15u - R.off - home >= 5u;   // outside home (points and bar)
 }
-// node after the path's steps (abs sources, in order) and the sources the
-// path rules out: movable at an earlier step and below that step's source
-BGX_DEV Node path_node(const Root& R, uint32_t path, int d, uint32_t okd, uint32_t& bad) {
+// node after the path's steps (abs sources, in order), its occupancy mask
+// (kept up to date per step: the source empties when it held one checker, the
+// destination fills) and the sources the path rules out: movable at an earlier
+// step and below that step's source
+BGX_DEV Node path_node(const Root& R, uint32_t path, int d, uint32_t okd, uint32_t& bad, uint32_t& occ) {
     Node n = root_node(R);
     bad = 0u;
+    occ = occ24(R.m0, R.m1, R.m2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t f = (path >> (5 * i)) & 31u;
         if (f != 31u) {
-            if (f < 24u) bad |= occ24(n.m0, n.m1, n.m2) & okd & ((1u << f) - 1u);
+            int dst;
+            if (f < 24u) {
+                bad |= occ & okd & ((1u << f) - 1u);
+                if (nib(n.m0, n.m1, n.m2, (int)f) == 1u) occ &= ~(1u << f);
+                dst = R.player == 0 ? (int)f + d : (int)f - d;
+            } else {
+                dst = R.player == 0 ? d - 1 : 24 - d;
+            }
             n = apply_move(R, n, (int)f, d);
+            if (dst >= 0 && dst <= 23) occ |= 1u << dst;
         }
     }
     return n;
+}
+// a node's move list in a path-mode job (no node of its tree can be in
+// bear-off: doubles_by_path): the bar entry while on the bar, else every
+// occupied point whose destination is open (get_moves_bar / get_moves_normal,
+// get_moves_one_die.py:40-130) -- node_moves without the bear-off analysis
+BGX_DEV Moves path_moves(const Root& R, const Node& n, uint32_t occ, int d, uint32_t okd) {
+    Moves mv;
+    mv.src = 0; mv.nsrc = 0; mv.e0 = -1; mv.e1 = -1; mv.n = 0;
+    if ((n.x & 15u) > 0u) {
+        const int entry = R.player == 0 ? d - 1 : 24 - d;
+        if (!((R.block >> entry) & 1u)) { mv.e0 = 24; mv.n = 1; }
+        return mv;
+    }
+    mv.src = occ & okd;
+    mv.nsrc = __popc(mv.src);
+    mv.n = mv.nsrc;
+    return mv;
 }
 BGX_DEV Node path_board(const Root& R, uint32_t path, int d) {
     Node n = root_node(R);
@@ -273,55 +301,69 @@ struct JobIn { Root R; int d0, d1; bool skip; };
 BGX_DEV JobIn make_job(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6,
                        int player, int d0, int d1);
 
-BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) {
-    JobIn in;
-    uint32_t w0, w1, w2, w3, w4, w5, w6;
-    int player = 0;
-    in.skip = false;
+// A job's input as loaded (fetch_raw), before the root analysis (decode_job):
+// the split lets a kernel load the next job's words while the current one runs.
+// IN_TWOPLY rows whose word 7 is SKIP_ROW are skipped (a lane with fewer than
+// four candidates, two_ply.py:67-70 via the engine's top-k).
+constexpr uint32_t SKIP_ROW = 0xFFFFFFFFu;
+struct RawJob { uint4 x, y; int player, d0, d1; };
+
+BGX_DEV RawJob fetch_raw(const MovegenArgs& a, int j) {
+    RawJob r;
+    r.player = 0;
+    r.d0 = r.d1 = 0;
     if (a.in_mode == IN_U8) {
         const uint32_t* b = (const uint32_t*)(a.in_u8 + (size_t)j * 52);
-        w0 = pack4(b[0]) | (pack4(b[1]) << 16);
-        w1 = pack4(b[2]) | (pack4(b[3]) << 16);
-        w2 = pack4(b[4]) | (pack4(b[5]) << 16);
-        w3 = pack4(b[6]) | (pack4(b[7]) << 16);
-        w4 = pack4(b[8]) | (pack4(b[9]) << 16);
-        w5 = pack4(b[10]) | (pack4(b[11]) << 16);
+        r.x = make_uint4(pack4(b[0]) | (pack4(b[1]) << 16), pack4(b[2]) | (pack4(b[3]) << 16),
+                         pack4(b[4]) | (pack4(b[5]) << 16), pack4(b[6]) | (pack4(b[7]) << 16));
         const uint32_t t = b[12];
-        w6 = (t & 15u) | (((t >> 8) & 15u) << 4) | (((t >> 16) & 15u) << 8) | (((t >> 24) & 15u) << 12);
-        player = a.in_player[j];
-        in.d0 = a.in_dice[2 * j];
-        in.d1 = a.in_dice[2 * j + 1];
-    } else {
-        int src = j;
-        if (a.in_mode == IN_TWOPLY) {
-            const int row = j / 21;
-            src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
-            if (src < 0) {
-                in.skip = true;
-                src = 0;
-            }
-        }
-        const uint4* p = (const uint4*)(a.in_packed + (size_t)src * 8);
-        const uint4 x = p[0], y = p[1];
-        w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w; w4 = y.x; w5 = y.y; w6 = y.z;
-        if (a.in_mode == IN_TWOPLY) {
-            // two_ply.py:93-150: the opponent of the candidate's mover replies to every roll
-            player = 1 - (int)((w6 >> 16) & 1u);
-            int a0 = 1, r = j - 21 * (j / 21);   // DICE_ROLLS order (two_ply.py:10-32)
-            while (r >= 7 - a0) { r -= 7 - a0; ++a0; }
-            in.d0 = a0;
-            in.d1 = a0 + r;
-        } else {
-            player = a.in_player[j];
-            in.d0 = a.in_dice[2 * j];
-            in.d1 = a.in_dice[2 * j + 1];
-        }
+        r.y = make_uint4(pack4(b[8]) | (pack4(b[9]) << 16), pack4(b[10]) | (pack4(b[11]) << 16),
+                         (t & 15u) | (((t >> 8) & 15u) << 4) | (((t >> 16) & 15u) << 8) | (((t >> 24) & 15u) << 12),
+                         0u);
+        r.player = a.in_player[j];
+        r.d0 = a.in_dice[2 * j];
+        r.d1 = a.in_dice[2 * j + 1];
+        return r;
     }
-    const bool skip = in.skip;
-    in = make_job(w0, w1, w2, w3, w4, w5, w6, player, in.d0, in.d1);
-    in.skip = skip;
+    int src = j;
+    if (a.in_mode == IN_TWOPLY) {
+        const int row = j / 21;
+        src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
+    }
+    if (src < 0) {
+        r.x = make_uint4(0, 0, 0, 0);
+        r.y = make_uint4(0, 0, 0, SKIP_ROW);
+    } else {
+        const uint4* p = (const uint4*)(a.in_packed + (size_t)src * 8);
+        r.x = p[0];
+        r.y = p[1];
+    }
+    if (a.in_mode != IN_TWOPLY) {
+        r.player = a.in_player[j];
+        r.d0 = a.in_dice[2 * j];
+        r.d1 = a.in_dice[2 * j + 1];
+    }
+    return r;
+}
+
+BGX_DEV JobIn decode_job(const MovegenArgs& a, int j, const RawJob& r) {
+    int player = r.player, d0 = r.d0, d1 = r.d1;
+    bool skip = false;
+    if (a.in_mode == IN_TWOPLY) {
+        skip = r.y.w == SKIP_ROW;
+        // two_ply.py:93-150: the opponent of the candidate's mover replies to every roll
+        player = 1 - (int)((r.y.z >> 16) & 1u);
+        int a0 = 1, q = j - 21 * (j / 21);   // DICE_ROLLS order (two_ply.py:10-32)
+        while (q >= 7 - a0) { q -= 7 - a0; ++a0; }
+        d0 = a0;
+        d1 = a0 + q;
+    }
+    JobIn in = make_job(r.x.x, r.x.y, r.x.z, r.x.w, r.y.x, r.y.y, r.y.z, player, d0, d1);
+    in.skip = uniform(skip ? 1 : 0) != 0;
     return in;
 }
+
+BGX_DEV JobIn fetch_job(const MovegenArgs& a, int j) { return decode_job(a, j, fetch_raw(a, j)); }
 
 // job from a packed board's words 0..6, the mover and the dice
 BGX_DEV JobIn make_job(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint32_t w5, uint32_t w6,
@@ -383,7 +425,9 @@ BGX_DEV int job_count(const MovegenArgs& a) {
 // Per-wave output reservation for OUT_PACKED_FLAT: one global atomic per
 // `flat_chunk` rows instead of one per job (a single counter hit by every job
 // of a 2-ply launch serialises at the memory side).
-struct FlatCursor { int base = 0, left = 0; };
+// left_hint >= 0: the jobs this wave still expects (kernels that do not
+// stride by gridDim.x set it per job; begin_emit sizes its reservation by it)
+struct FlatCursor { int base = 0, left = 0, left_hint = -1; };
 
 // reserve output space once the job's record count is known; returns base (-1: overflow)
 BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
@@ -395,7 +439,8 @@ BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
             fc.left -= n;
         } else {
             // chunk = min(flat_chunk, 32 rows per job this wave still has), at least n
-            const int left_jobs = (job_count(a) - j + (int)gridDim.x - 1) / (int)gridDim.x;
+            const int left_jobs =
+                fc.left_hint >= 0 ? fc.left_hint : (job_count(a) - j + (int)gridDim.x - 1) / (int)gridDim.x;
             int want = 32 * left_jobs;
             if (want > a.flat_chunk) want = a.flat_chunk;
             const int grab = n > want ? n : want;
@@ -555,7 +600,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         mA.e1 = pass ? mL.e1 : mH.e1;
         mA.n = pass ? mL.n : mH.n;
         int s1 = 0;
-        if (v1) s1 = move_source(mA, k);
+        if (v1) s1 = k < mA.nsrc ? select_bit_fast(mA.src, k) : (k == mA.nsrc ? mA.e0 : mA.e1);
         const Node child = v1 ? apply_move(R, root, s1, dA) : root;
         Moves m2 = node_moves(R, child, dB, pass ? okH : okL);
         const int c = v1 ? m2.n : 0;
@@ -638,9 +683,9 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                     const int i = b + l;
                     const bool live = i < n;
                     const uint32_t path = live ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
-                    uint32_t bad;
-                    const Node nd = path_node(R, path, d, okd, bad);
-                    Moves pm = node_moves(R, nd, d, okd);
+                    uint32_t bad, occ;
+                    const Node nd = path_node(R, path, d, okd, bad, occ);
+                    Moves pm = path_moves(R, nd, occ, d, okd);
                     const uint32_t one = pm.n == 1 ? FLAG1 : 0u;
                     pm.src &= ~bad;                      // e0 is the bar entry (or none) here
                     pm.nsrc = __popc(pm.src);
@@ -838,8 +883,9 @@ BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
             if (hh * NTH + 64 * w < n) {        // wave-uniform
                 const int i = hh * NTH + t;
                 const uint32_t path = i < n ? fa[i] & KEYMASK : PATH_EMPTY;
-                uint32_t bad;
-                const Moves pm = node_moves(R, path_node(R, path, d, okd, bad), d, okd);
+                uint32_t bad, occ;
+                const Node nd = path_node(R, path, d, okd, bad, occ);
+                const Moves pm = path_moves(R, nd, occ, d, okd);
                 const uint32_t ok = pm.src & ~bad;
                 const int ns = __popc(ok);
                 c[hh] = i < n ? ns + (pm.e0 >= 0 ? 1 : 0) : 0;

@@ -57,6 +57,62 @@ __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
     }
 }
 
+// Tier 1 for large launches (the 2-ply replies), balanced: a workgroup of PW
+// waves owns a contiguous range of the jobs and its waves take the range's
+// next job from an LDS counter. With a static stride the launch lasts as long
+// as its unluckiest wave (67 jobs of very different cost each for the 344 k
+// reply jobs of a 4,096-lane K=4 step); here a wave that drew cheap jobs
+// takes more, and the 21 rolls of one candidate row stay on one CU (its L2).
+// The next job's board is loaded while the current job runs.
+constexpr int PW = 10;                                  // waves per workgroup (two per CU)
+constexpr int PF = Slice<S_T1>::F - 8;                  // frontier entries: 10 slices + the counter in 80 KB
+constexpr int PSL = S_T1 * 8 + 2 * PF * 4 + 64 * 4;     // slice bytes
+static_assert(PW * PSL + 16 <= 80 * 1024, "two workgroups per CU");
+
+__global__ __launch_bounds__(64 * PW) void movegen_pool_kernel(MovegenArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
+    __shared__ int next_job;
+    const int w = (int)threadIdx.x >> 6, l = lane_id();
+    unsigned long long* sl = smem + (size_t)w * (PSL / 8);
+    Mem M;
+    M.tab = sl;
+    M.S = S_T1;
+    M.F = PF;
+    M.fa = (uint32_t*)(sl + S_T1);
+    M.fb = M.fa + PF;
+    M.map = M.fb + PF;
+    M.exp = a.exp_mode;
+    M.map[l] = 0u;
+    const int n_jobs = uniform(job_count(a));
+    // the workgroup's jobs are b, b + G, b + 2G, ... (a contiguous range would
+    // hold the rolls of only ~8 root positions, whose costs are correlated);
+    // its waves take them in order from the counter
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int nk = n_jobs > b ? (n_jobs - b + G - 1) / G : 0;
+    if (threadIdx.x == 0) next_job = PW;
+    __syncthreads();
+    FlatCursor fc;
+    int k = w;
+    RawJob raw;
+    if (k < nk) raw = fetch_raw(a, b + k * G);
+    while (k < nk) {   // k is wave-uniform
+        int kn = 0;
+        if (l == 0) kn = atomicAdd(&next_job, 1);
+        kn = uniform(kn);
+        const int j = b + k * G;
+        const JobIn in = decode_job(a, j, raw);
+        if (kn < nk) raw = fetch_raw(a, b + kn * G);
+        fc.left_hint = (nk - k + PW - 1) / PW;
+        if (in.skip) {
+            begin_emit(a, j, 0, fc);
+        } else {
+            const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc, a.heavy_t);
+            if (r < 0 && l == 0) push_ovf(a, j);
+        }
+        k = kn;
+    }
+}
+
 // Tier 1 for launches with few jobs (the 1-ply step, the first 2-ply launch):
 // 16-wave blocks, one job per wave per window. The block reserves its rows of
 // the flat output with ONE atomic (a same-address global atomic costs ~11 ns
@@ -216,12 +272,13 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         if (e != hipSuccess) return e;
     }
     // resident blocks per CU of each kernel (LDS, registers, 32 waves)
-    static int per_cu1 = 0, per_cub = 0, per_cuf = 0;
+    static int per_cu1 = 0, per_cub = 0, per_cuf = 0, per_cup = 0;
     if (!per_cu1) {
         auto occ = [](int& n, const void* k, int threads, int dflt) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n <= 0) n = dflt;
         };
         occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 64, 20);
+        occ(per_cup, (const void*)bgx::movegen_pool_kernel, 64 * bgx::PW, 2);
         occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
         occ(per_cuf, (const void*)bgx::movegen_few_kernel, bgx::NTH, 1);
     }
@@ -237,6 +294,10 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     if (const char* v = getenv("BGX_MG_FEW")) fewm = atoi(v);
     const bool few_jobs = !a.n_jobs_dev && a.n_jobs <= n_cu * per_cuf * bgx::BW * 4;
     const bool few = fewm == 1 || (fewm < 0 && few_jobs);
+    // large launches: the balanced pool kernel (BGX_MG_POOL=0: the strided per-wave kernel)
+    int poolm = 1;
+    if (const char* v = getenv("BGX_MG_POOL")) poolm = atoi(v);
+    const bool pool = poolm != 0;
     int heavy = bgx::HEAVY_T;
     if (const char* v = getenv("BGX_MG_HEAVY_T")) heavy = atoi(v);
     // heavy doubles go to the block-cooperative tier 2 when the launch is
@@ -250,6 +311,12 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         int blocks = a.n_jobs_dev ? n_cu * per_cuf : (a.n_jobs + bgx::BW - 1) / bgx::BW;
         if (blocks > n_cu * per_cuf) blocks = n_cu * per_cuf;
         hipLaunchKernelGGL(bgx::movegen_few_kernel, dim3(blocks), dim3(bgx::NTH), 0, stream, a);
+    } else if (pool) {
+        // balanced tier 1: 10-wave workgroups over contiguous job ranges
+        int blocks = n_cu * per_cup;
+        const int need = (a.n_jobs + bgx::PW - 1) / bgx::PW;
+        if (!a.n_jobs_dev && need < blocks) blocks = need;
+        hipLaunchKernelGGL(bgx::movegen_pool_kernel, dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
     } else {
         int blocks = n_cu * per_cu1;
         if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;

@@ -292,6 +292,52 @@ def test_fused_step_matches_phased_engine(weights_seed0, tier, monkeypatch):
         assert st["fallback_jobs"] > 0
 
 
+def test_2ply_tier1_kernels_agree(weights_seed0, monkeypatch):
+    """2-ply K=4 (128 lanes: 10,752 reply jobs per step) with the reply launch
+    on the 16-wave block kernel (BGX_MG_FEW=1), the balanced pool kernel (the
+    default for large launches) and the strided per-wave kernel
+    (BGX_MG_POOL=0): identical episodes and records (the reply rows land at
+    different flat offsets; V, the top-5 means and the picks do not change)."""
+    runs = []
+    for few, pool in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("BGX_MG_FEW", few)
+        monkeypatch.setenv("BGX_MG_POOL", pool)
+        e = _engine(weights_seed0, lanes=128, seed=5, ply=2, k_top=4)
+        runs.append(_by_episode(*_collect(e, 60, chunk=30)))
+        e.close()
+    _same_runs(runs[0], runs[1])
+    _same_runs(runs[0], runs[2])
+
+
+@pytest.mark.parametrize("pref,skip", [("0", "0"), ("1", "1")])
+def test_reply_mlp_variants_keep_v_bits(weights_seed0, pref, skip, monkeypatch):
+    """The throughput MLP kernel with / without the row prefetch and the
+    zero-k-step skip: the 2-ply engine's records are bit-identical to a run of
+    the default build (the skip adds exact zeros; the order of the sums is
+    fixed). Each variant runs in its own process (the choice is read once)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO as REPO_ROOT
+    code =("import sys, json, numpy as np; sys.path[:0] = ['tests', 'mlp-ppo-2ply-multi_amd', 'oracle'];"
+            "import test_gpu_engine as t; from conftest import golden;"
+            "w = {k: golden('weights_seed0.npz')[k] for k in ('W1', 'b1', 'w2', 'b2')};"
+            "e = t._engine(w, lanes=128, seed=8, ply=2, k_top=4); h, r = t._collect(e, 40, chunk=40);"
+            "print(json.dumps([float(np.asarray(d['v_a'], np.float64).sum()) for d in r] +"
+            " [float(np.asarray(d['v_s'], np.float64).sum()) for d in r] + [int(len(d['action'])) for d in r]))")
+    outs = []
+    for env in ({"BGX_MLP_PREF": pref, "BGX_MLP_SKIP": skip}, {}):
+        full = dict(os.environ)
+        full.pop("BGX_MLP_PREF", None)
+        full.pop("BGX_MLP_SKIP", None)
+        full.update(env)
+        res = subprocess.run([sys.executable, "-c", code], cwd=REPO_ROOT, env=full, capture_output=True, text=True,
+                             timeout=300)
+        assert res.returncode == 0, res.stderr[-2000:]
+        outs.append(res.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1]
+
+
 def test_fused_greedy_and_ragged_lanes(weights_ckpt):
     """A lane count that is not a multiple of 16 (the last workgroup is partly
     empty) and greedy play: fused == phased on the shipped checkpoint."""

@@ -32,15 +32,17 @@ def _run_movegen(ops, boards, player, dice, cap):
     return out.cpu().numpy(), cnt.cpu().numpy()
 
 
-# tier-1 kernel (per-wave "0" / 16-wave block "1") x heavy-doubles hand-off to
-# the block-cooperative tier 2 (off "0" / on "1")
-MG_MODES = [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")]
+# tier-1 kernel (large-launch "0" / 16-wave block "1") x heavy-doubles
+# hand-off to the block-cooperative tier 2 (off "0" / on "1") x the
+# large-launch kernel: balanced pool "1" (default) / strided per-wave "0"
+MG_MODES = [("0", "0", "1"), ("0", "0", "0"), ("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")]
 
 
-@pytest.mark.parametrize("few,coop", MG_MODES)
-def test_movegen_golden_cases(bgx_ops, few, coop, monkeypatch):
+@pytest.mark.parametrize("few,coop,pool", MG_MODES)
+def test_movegen_golden_cases(bgx_ops, few, coop, pool, monkeypatch):
     monkeypatch.setenv("BGX_MG_FEW", few)
     monkeypatch.setenv("BGX_MG_COOP", coop)
+    monkeypatch.setenv("BGX_MG_POOL", pool)
     d = golden("movegen_cases.npz")
     out, cnt = _run_movegen(bgx_ops, d["boards"], d["player"], d["dice"], cap=1024)
     for i in range(len(d["boards"])):
@@ -91,10 +93,11 @@ def _fuzz_positions(seed, n_games):
     return pos
 
 
-@pytest.mark.parametrize("few,coop", [("0", "0"), ("1", "1")])
-def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, few, coop, monkeypatch):
+@pytest.mark.parametrize("few,coop,pool", [("0", "0", "1"), ("0", "0", "0"), ("1", "1", "1")])
+def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, few, coop, pool, monkeypatch):
     monkeypatch.setenv("BGX_MG_FEW", few)
     monkeypatch.setenv("BGX_MG_COOP", coop)
+    monkeypatch.setenv("BGX_MG_POOL", pool)
     pos = _fuzz_positions(1234, 40)
     rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
     boards = np.stack([p[0] for p in pos for _ in rolls])
