@@ -210,7 +210,7 @@ def roofline_for(d, tm, leg):
     dom = "movegen" if mg_ms >= mlp_ms else "mlp"
     r = {k: out[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
     r["kernel"] = ({"1ply": "movegen launch = bgx::movegen_few_kernel + bgx::movegen_block_kernel",
-                    "2ply": "movegen launches = (few | lds<512>) + bgx::movegen_block_kernel"}[leg]
+                    "2ply": "movegen launches = (few | pool) + bgx::movegen_block_kernel"}[leg]
                    if dom == "movegen" else "bgx::mlp_kernel")
     r["traffic"] = None
     prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
