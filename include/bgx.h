@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 3
+#define BGX_ABI_VERSION 4
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -78,6 +78,14 @@ int bgx_value_boards(const bgx_net* net, const uint8_t* d_boards, const uint8_t*
 int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
                 double* d_out, void* stream);
 
+/* bgx_two_ply in the reference-sampled mode (multi/two_ply.py:119-121): for
+ * the rolls 1-1, 2-2 and 3-3 a reply set larger than sample_k (the reference:
+ * 50) is replaced by a uniformly random sample_k of its replies
+ * (random.sample; here a keyed permutation, reproducible per seed) before the
+ * top-5 mean. sample_k = 0 is the exact mode (= bgx_two_ply). */
+int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
+                        int sample_k, uint64_t seed, double* d_out, void* stream);
+
 /* ---------------- self-play engine ---------------- */
 typedef struct bgx_engine bgx_engine;
 
@@ -99,6 +107,8 @@ typedef struct bgx_config {
     int fused;              /* 1-ply only, 1 (default): bgx_step runs as ONE persistent launch in which
                                each 16-lane workgroup advances its lanes through all n_steps (movegen,
                                MLP, select, step fused; same results as 0 = one launch per phase) */
+    int reply_sample;       /* 2-ply: 0 (default) = exact mode; 50 = the reference's random.sample of 50
+                               replies for 1-1 / 2-2 / 3-3 (two_ply.py:119-121), keyed by seed + step */
 } bgx_config;
 
 void bgx_config_default(bgx_config* cfg);

@@ -38,7 +38,7 @@ class Harvest:
 class Engine:
     def __init__(self, lanes=4096, seed=0, ply=1, k_top=4, device=None, lane_base=0, alpha=1.0,
                  beta=0.9, max_steps=300, max_legal=500, ring=640, ep_cap=0, cand_per_lane=256,
-                 reply_per_lane=0, greedy=False, fused=True):
+                 reply_per_lane=0, greedy=False, fused=True, reply_sample=0):
         require_cuda()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         cfg = Config()
@@ -49,6 +49,7 @@ class Engine:
         cfg.cand_per_lane, cfg.reply_per_lane = int(cand_per_lane), int(reply_per_lane)
         cfg.greedy = 1 if greedy else 0
         cfg.fused = 1 if fused else 0   # 1-ply: one persistent launch per step() call
+        cfg.reply_sample = int(reply_sample)   # 2-ply: 0 exact, 50 = two_ply.py:119-121 random.sample
         self.cfg = cfg
         self.lanes = int(lanes)
         self.fused = bool(fused) and int(ply) == 1

@@ -138,14 +138,16 @@ class Net:
                                      stream_handle(stream)), "bgx_value_boards")
         return out
 
-    def two_ply(self, boards, opponent, stream=None):
-        """Exact-mode compute_weighted_opponent_response (two_ply.py:93-150) for
-        afterstates [n, 52]; returns float64 W [n]."""
+    def two_ply(self, boards, opponent, sample=0, seed=0, stream=None):
+        """compute_weighted_opponent_response (two_ply.py:93-150) for afterstates
+        [n, 52]; returns float64 W [n]. sample=0: exact mode; sample=50: the
+        reference's random.sample of 50 replies for 1-1 / 2-2 / 3-3
+        (two_ply.py:119-121), reproducible per seed."""
         boards, opponent = _u8(boards).view(-1, 52), _u8(opponent).view(-1)
         require_cuda(boards, opponent)
         out = torch.empty((boards.shape[0],), dtype=torch.float64, device=boards.device)
-        check(lib().bgx_two_ply(self._h, ptr(boards), ptr(opponent), boards.shape[0], ptr(out),
-                                stream_handle(stream)), "bgx_two_ply")
+        check(lib().bgx_two_ply_sampled(self._h, ptr(boards), ptr(opponent), boards.shape[0], int(sample),
+                                        int(seed), ptr(out), stream_handle(stream)), "bgx_two_ply_sampled")
         return out
 
 

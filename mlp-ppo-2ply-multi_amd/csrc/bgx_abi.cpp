@@ -308,7 +308,14 @@ int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t
 
 int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
                 double* d_out, void* stream) {
+    return bgx_two_ply_sampled(net, d_boards, d_opponent, n, 0, 0, d_out, stream);
+}
+
+int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
+                        int sample_k, uint64_t seed, double* d_out, void* stream) {
     if (!net || n < 0) return fail(BGX_E_ARG, "bgx_two_ply: bad arguments");
+    if (sample_k != 0 && (sample_k < 5 || sample_k > 1024))
+        return fail(BGX_E_ARG, "bgx_two_ply_sampled: sample_k=%d (0 = exact, 5..1024)", sample_k);
     if (n == 0) return BGX_OK;
     if (!d_boards || !d_opponent || !d_out) return fail(BGX_E_ARG, "bgx_two_ply: null pointer");
     hipStream_t s = (hipStream_t)stream;
@@ -375,7 +382,8 @@ int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_op
         m.feat_scale = net->feat_scale;
         if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
     }
-    if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, s) != hipSuccess) rc = BGX_E_HIP;
+    if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, sample_k, seed, nullptr, s) != hipSuccess)
+        rc = BGX_E_HIP;
     if (!rc && bgx_launch_two_ply_reduce(jv, n, d_out, s) != hipSuccess) rc = BGX_E_HIP;
     unsigned flags = 0;
     if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
@@ -449,6 +457,8 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     if (cfg->ply != 1 && cfg->ply != 2) return fail(BGX_E_ARG, "ply=%d (1 or 2)", cfg->ply);
     if (cfg->ply == 2 && cfg->k_top != 4 && cfg->k_top != 0)
         return fail(BGX_E_ARG, "k_top=%d (4 = reference, 0 = all)", cfg->k_top);
+    if (cfg->reply_sample != 0 && (cfg->reply_sample < 5 || cfg->reply_sample > 1024))
+        return fail(BGX_E_ARG, "reply_sample=%d (0 = exact, 5..1024; the reference samples 50)", cfg->reply_sample);
     if (cfg->max_steps <= 0 || cfg->max_legal <= 0) return fail(BGX_E_ARG, "max_steps/max_legal");
     if (cfg->ring < cfg->max_steps + 1) return fail(BGX_E_ARG, "ring=%d < max_steps+1", cfg->ring);
     HIP_TRY(hipSetDevice(device));
@@ -686,12 +696,15 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             if (timed(e, 1, s, true)) return BGX_E_HIP;
             HIP_TRY(bgx_launch_mlp(&r, s));
             if (timed(e, 1, s, false)) return BGX_E_HIP;
+            // reference-sampled mode (cfg.reply_sample > 0): keyed by the seed and the
+            // lane block, salted per step by the engine's env-step counter
+            const uint64_t skey = e->cfg.seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(e->cfg.lane_base + 1));
             if (e->cfg.k_top == 4) {
                 HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, L * 4 * 21, nullptr, 0, L * 4 * 21,
-                                        e->job_val, s));
+                                        e->job_val, e->cfg.reply_sample, skey, e->stats, s));
             } else {
                 HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, 0, e->ctr + C_FLAT, 21, e->jobs_cap,
-                                        e->job_val, s));
+                                        e->job_val, e->cfg.reply_sample, skey, e->stats, s));
             }
         }
         HIP_TRY(bgx_launch_select(&e->d, s));   // select + env step (one launch)

@@ -166,19 +166,55 @@ __global__ __launch_bounds__(256) void topk_kernel(EngineDev e) {
     }
 }
 
+// two_ply.py:119-121, reference-sampled mode: a 1-1 / 2-2 / 3-3 job with more
+// than sample_k replies keeps a uniformly random sample_k of them
+// (random.sample). Reply k is kept iff pi(k) < sample_k, pi a pseudo-random
+// permutation of [0, c): a 4-round Feistel network on 10 bits, round keys
+// from Philox per (job, step), cycle-walked into [0, c) (c <= 1024; the
+// largest reply count seen is 667).
+BGX_DEV uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    return x ^ (x >> 16);
+}
+BGX_DEV uint32_t perm_below(uint32_t x, uint32_t c, const u32x4& key) {
+    const uint32_t ks[4] = {key.x, key.y, key.z, key.w};
+    do {
+        uint32_t L = x >> 5, R = x & 31u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t t = L ^ (mix32(R ^ ks[r]) & 31u);
+            L = R;
+            R = t;
+        }
+        x = (L << 5) | R;
+    } while (x >= c);
+    return x;
+}
+BGX_DEV bool small_double(int j) {   // DICE_ROLLS index 0 = 1-1, 6 = 2-2, 11 = 3-3 (two_ply.py:10-32)
+    const int r = j % 21;
+    return r == 0 || r == 6 || r == 11;
+}
+
 // 2-ply: per (candidate, roll) job, mean of the top-5 reply values
 // (two_ply.py:133-142); 0 when the opponent has no move (the roll adds nothing).
 // 16 lanes per job (coalesced loads); each lane keeps its top 5, then five
 // group-max rounds pop the job's top 5 in descending order (the reference's
-// summation order).
+// summation order). sample_k > 0: the reference-sampled mode above, keyed by
+// skey and the step salt *salt_dev (null: 0).
 __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    const int32_t* __restrict__ job_off,
                                                    const int32_t* __restrict__ job_cnt, int n_jobs,
                                                    const unsigned* __restrict__ n_units_dev,
-                                                   int jobs_per_unit, int max_jobs, float* __restrict__ out) {
+                                                   int jobs_per_unit, int max_jobs, float* __restrict__ out,
+                                                   int sample_k, uint64_t skey,
+                                                   const unsigned long long* __restrict__ salt_dev) {
     int nj = n_jobs;
     if (n_units_dev) nj += (int)(*n_units_dev) * jobs_per_unit;
     if (nj > max_jobs) nj = max_jobs;
+    const unsigned long long salt = (sample_k > 0 && salt_dev) ? *salt_dev : 0ull;
     const int gl = lane_id() & 15, q = lane_id() >> 4;
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int n_waves = (int)((gridDim.x * blockDim.x) >> 6);
@@ -187,9 +223,14 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
     for (int jb = 4 * wave; jb < nj; jb += 4 * n_waves) {
         const int j = jb + q;
         const bool live = j < nj;
-        const int c = live ? job_cnt[j] : 0, o = live ? job_off[j] : 0;
+        int c = live ? job_cnt[j] : 0;
+        const int o = live ? job_off[j] : 0;
+        const bool samp = sample_k > 0 && c > sample_k && c <= 1024 && small_double(j);
+        u32x4 pk = {0u, 0u, 0u, 0u};
+        if (samp) pk = philox(skey, 0x2B1A000000000000ull ^ salt, (uint64_t)j);
         float t[5] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
         for (int k = gl; k < c; k += 16) {
+            if (samp && perm_below((uint32_t)k, (uint32_t)c, pk) >= (uint32_t)sample_k) continue;
             const float v = V[o + k];
             if (!(v > t[4])) continue;
             if (v > t[0]) { t[4] = t[3]; t[3] = t[2]; t[2] = t[1]; t[1] = t[0]; t[0] = v; }
@@ -198,6 +239,7 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
             else if (v > t[3]) { t[4] = t[3]; t[3] = v; }
             else { t[4] = v; }
         }
+        if (samp) c = sample_k;   // the replies kept
         const int m = c < 5 ? c : 5;
         float s = 0.0f;
         for (int r = 0; r < 5; ++r) {
@@ -302,12 +344,13 @@ extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t strea
 }
 extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt,
                                       int n_jobs, const unsigned* n_units_dev, int jobs_per_unit,
-                                      int max_jobs, float* out, hipStream_t stream) {
+                                      int max_jobs, float* out, int sample_k, uint64_t skey,
+                                      const unsigned long long* salt_dev, hipStream_t stream) {
     if (max_jobs <= 0) return hipSuccess;
     int blocks = (max_jobs + 15) / 16;   // 16 jobs per 256-thread block
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
-                       n_units_dev, jobs_per_unit, max_jobs, out);
+                       n_units_dev, jobs_per_unit, max_jobs, out, sample_k, skey, salt_dev);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out,

@@ -152,7 +152,7 @@ hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream);
 hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream);   // select + env step
 hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt, int n_jobs,
                            const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
-                           hipStream_t stream);
+                           int sample_k, uint64_t skey, const unsigned long long* salt_dev, hipStream_t stream);
 hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out, hipStream_t stream);
 hipError_t bgx_launch_harvest(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* out,
                               hipStream_t stream);

@@ -176,6 +176,64 @@ def test_two_ply_exact_mode_vs_reference(weights_seed0, weights_ckpt):
         np.testing.assert_allclose(W.cpu().numpy(), t[key], atol=V_TOL, rtol=0)
 
 
+ROLLS21 = [(a, b) for a in range(1, 7) for b in range(a, 7)]   # DICE_ROLLS order (two_ply.py:10-32)
+P21 = np.array([1.0 if a == b else 2.0 for a, b in ROLLS21]) / 36.0
+SMALL_DOUBLES = (0, 6, 11)                                      # 1-1, 2-2, 3-3 (two_ply.py:119-121)
+
+
+def _reply_values(weights, board, opp, r):
+    a, b = ROLLS21[r]
+    n, res, _ = orc.movegen(board, opp, a, b)
+    return orc.value(weights, orc.encode_many(res, [opp] * n)) if n else np.zeros(0)
+
+
+def test_two_ply_reference_sampled_mode(weights_seed0):
+    """two_ply.py:119-121 (random.sample of 50 replies for 1-1 / 2-2 / 3-3) as
+    bgx_two_ply_sampled: reproducible per seed; equal to the exact mode where
+    no such roll has more than 50 replies; never above it (a subset's top-5
+    mean is at most the full set's); its mean over seeds matches the mean over
+    numpy random 50-subsets of the oracle's reply values."""
+    from bgx import ops
+    t = golden("two_ply.npz")
+    net = ops.Net(weights_seed0)
+    B, O = torch.from_numpy(t["boards"]).cuda(), torch.from_numpy(t["opponent"]).cuda()
+    exact = net.two_ply(B, O).cpu().numpy()
+    s = net.two_ply(B, O, sample=50, seed=3).cpu().numpy()
+    np.testing.assert_array_equal(s, net.two_ply(B, O, sample=50, seed=3).cpu().numpy())
+    assert np.all(s <= exact + 1e-12)
+    affected = []
+    for i in range(len(exact)):
+        big = [r for r in SMALL_DOUBLES
+               if len(_reply_values(weights_seed0, t["boards"][i], int(t["opponent"][i]), r)) > 50]
+        if big:
+            affected.append((i, big))
+        else:
+            assert s[i] == exact[i], i
+    assert affected, "the fixture holds positions with > 50 replies to a small double"
+    rng = np.random.default_rng(0)
+    for i, big in affected[:2]:
+        seeds = 200
+        draws = net.two_ply(B[i:i + 1].repeat(seeds, 1), O[i:i + 1].repeat(seeds), sample=50, seed=11).cpu().numpy()
+        assert len(np.unique(draws)) > 1   # jobs of the batch draw different subsets
+        mu, var = exact[i], 0.0
+        for r in big:
+            v = _reply_values(weights_seed0, t["boards"][i], int(t["opponent"][i]), r)
+            full = np.sort(v)[::-1][:5].mean()
+            sub = np.array([np.sort(rng.choice(v, 50, replace=False))[::-1][:5].mean() for _ in range(3000)])
+            mu += P21[r] * (sub.mean() - full)
+            var += P21[r] ** 2 * sub.var()
+        assert abs(draws.mean() - mu) < 5 * np.sqrt(var / seeds) + 1e-6, (i, draws.mean(), mu, np.sqrt(var / seeds))
+
+
+def test_engine_2ply_reference_sampled_mode(weights_seed0):
+    """Engine(reply_sample=50): the reference-sampled 2-ply keeps every
+    transition valid and the chosen action among the top-4 by 1-ply V."""
+    e = _engine(weights_seed0, lanes=64, seed=4, ply=2, k_top=4, reply_sample=50)
+    hdrs, recs = _collect(e, 60, chunk=30)
+    e.close()
+    assert _check_transitions(weights_seed0, hdrs, recs, 2) > 200
+
+
 def _by_episode(hdrs, recs):
     """{(lane, episode no.): (header words 2.., {field: records})} — header
     order is the device's atomic append order, so runs compare per episode."""
