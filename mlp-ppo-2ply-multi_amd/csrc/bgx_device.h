@@ -339,6 +339,26 @@ BGX_DEV float wave_incl_maxf(float v) {
     v = dpp_maxf<0x143, 0xC>(v);
     return v;
 }
+// half-wave (lanes 32h .. 32h + 31) versions: row_shr within 16-lane rows,
+// then row_bcast:15 into rows 1 and 3 (no row_bcast:31, which crosses halves)
+BGX_DEV float half_incl_scanf(float v) {
+    v = dpp_addf<0x111, 0xF>(v);
+    v = dpp_addf<0x112, 0xF>(v);
+    v = dpp_addf<0x114, 0xF>(v);
+    v = dpp_addf<0x118, 0xF>(v);
+    v = dpp_addf<0x142, 0xA>(v);
+    return v;
+}
+BGX_DEV float half_incl_maxf(float v) {
+    v = dpp_maxf<0x111, 0xF>(v);
+    v = dpp_maxf<0x112, 0xF>(v);
+    v = dpp_maxf<0x114, 0xF>(v);
+    v = dpp_maxf<0x118, 0xF>(v);
+    v = dpp_maxf<0x142, 0xA>(v);
+    return v;
+}
+// the half-wave's lane 31 value (its inclusive total) to every lane of the half
+BGX_DEV float half_last(float v) { return __shfl(v, (lane_id() & 32) + 31, 64); }
 BGX_DEV int wave_sum(int v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -58,6 +58,34 @@ struct WaveRng {
     }
 };
 
+// The same stream drawn by a half-wave (two game lanes per wavefront, one
+// per half): lane k of the half evaluates counter base + k, draws come over
+// by shuffles within the half.
+struct HalfRng {
+    uint64_t key, ctr, base;
+    u32x4 batch;
+    BGX_DEV void refill() {
+        base = ctr;
+        batch = philox(key, 0x5EED0000ull, base + (uint64_t)(lane_id() & 31));
+    }
+    BGX_DEV u32x4 at(int k) const {   // counter base + k, k < 32 (uniform within the half)
+        const int src = (lane_id() & 32) + k;
+        return {(uint32_t)__shfl((int)batch.x, src, 64), (uint32_t)__shfl((int)batch.y, src, 64),
+                (uint32_t)__shfl((int)batch.z, src, 64), (uint32_t)__shfl((int)batch.w, src, 64)};
+    }
+    BGX_DEV u32x4 next() {
+        if (ctr - base >= 32u) refill();
+        const u32x4 r = at((int)(ctr - base));
+        ++ctr;
+        return r;
+    }
+    BGX_DEV void roll(int& a, int& b) {
+        u32x4 r = next();
+        a = die_from(r.x);
+        b = die_from(r.y);
+    }
+};
+
 // packed initial board (immutable_board.py:27-70): P1 {0:2, 11:5, 16:3, 18:5}, P2 {23:2, 12:5, 7:3, 5:5}
 BGX_DEV void initial_packed(uint32_t* w) {
     w[0] = 0x2u;                       // P1 point 0: 2
@@ -322,6 +350,51 @@ BGX_DEV int pick_action(X x, int m, bool greedy, float u) {
             break;
         }
         carry += lane63f(p);
+    }
+    return pick;
+}
+
+// pick_action over one half-wave (lanes 32h .. 32h + 31 choose for one game
+// lane, so a wavefront's two lanes choose side by side): softmax + inverse-CDF
+// sample at uniform u, or the argmax with greedy, as pick_action, with 32-lane
+// reductions. Every engine path uses this one, so the fused and phased
+// engines sum the same terms in the same order (identical picks).
+template <typename X>
+BGX_DEV int pick_action_half(X x, int m, bool greedy, float u) {
+    const int l = lane_id() & 31, hb = lane_id() & 32;
+    float mx = -INFINITY;
+    for (int k = l; k < m; k += 32) mx = fmaxf(mx, x(k));
+    mx = half_last(half_incl_maxf(mx));
+    float sum = 0.0f;
+    for (int k = l; k < m; k += 32) sum += __expf(x(k) - mx);
+    sum = half_last(half_incl_scanf(sum));
+    if (greedy) {
+        float bv = -INFINITY;
+        int bk = 0x7FFFFFFF;
+        for (int k = l; k < m; k += 32) {
+            const float xk = x(k);
+            if (xk > bv) { bv = xk; bk = k; }
+        }
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) {
+            const float ov = __shfl_xor(bv, off, 64);
+            const int ok = __shfl_xor(bk, off, 64);
+            if (ov > bv || (ov == bv && ok < bk)) { bv = ov; bk = ok; }
+        }
+        return bk;
+    }
+    int pick = m - 1;
+    const float t = u * sum;
+    float carry = 0.0f;
+    for (int b = 0; b < m; b += 32) {
+        const int k = b + l;
+        const float p = half_incl_scanf(k < m ? __expf(x(k) - mx) : 0.0f);
+        const uint32_t hit = (uint32_t)(ballot(k < m && t < carry + p) >> hb);
+        if (hit) {
+            pick = b + __ffs(hit) - 1;
+            break;
+        }
+        carry += half_last(p);
     }
     return pick;
 }

@@ -68,11 +68,12 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
         *e.ovf_count = 0u;
         *e.ovf_count2 = 0u;
     }
-    __shared__ float xs[4][512];
-    const int w = threadIdx.x >> 6;
-    const int i = blockIdx.x * 4 + w;
+    // one game lane per half-wave (8 per 256-thread block), as in the fused engine
+    __shared__ float xs[8][512];
+    const int slot = ((int)threadIdx.x >> 5);
+    const int i = blockIdx.x * 8 + slot;
     if (i >= e.L) return;
-    const int l = lane_id();
+    const int l = lane_id() & 31;
     const int n_full = e.cand_cnt[i];
     const int n = n_full < e.max_legal ? n_full : e.max_legal;
     if (n == 0) {
@@ -83,8 +84,8 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
     const float T = e.temperature;
     const bool k4 = e.ply == 2 && e.k_top == 4 && e.sel[4 * i] >= 0;
     const int m = k4 ? 4 : n;
-    float* x = xs[w];
-    for (int k = l; k < m; k += 64) {
+    float* x = xs[slot];
+    for (int k = l; k < m; k += 32) {
         float v;
         if (k4) {
             double W = 0.0;
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
         x[k] = v;
     }
     wave_sync();
-    const int pick = pick_action([&](int k) { return x[k]; }, m, e.greedy != 0, lane_uniform(e, i));
+    const int pick = pick_action_half([&](int k) { return x[k]; }, m, e.greedy != 0, lane_uniform(e, i));
     if (l == 0) step_lane(e, i, k4 ? e.sel[4 * i + pick] - base : pick);
 }
 
@@ -335,7 +336,7 @@ extern "C" hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream
 }
 
 extern "C" hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::select_step_kernel, dim3((e->L + 3) / 4), dim3(256), 0, stream, *e);
+    hipLaunchKernelGGL(bgx::select_step_kernel, dim3((e->L + 7) / 8), dim3(256), 0, stream, *e);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream) {

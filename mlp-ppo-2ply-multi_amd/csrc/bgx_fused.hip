@@ -271,30 +271,33 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
             tick(3);
             // ---- 5. action choice + env step for the wave's lanes (the chosen
             // afterstate is still staged in LDS when the step fit one MLP batch)
-            for (int q = 0; q < LPW; ++q) {
-                const int v = w * LPW + q;
-                if (v >= nlive) continue;
+            // (the wave's two lanes side by side, one per half-wave)
+            static_assert(LPW == 2, "one lane per half-wave");
+            {
+                const int v = w * LPW + (l >> 5);
+                const bool lead = (l & 31) == 0;
+                if (v < nlive) {
                 const int i = g * FL + v;
                 const unsigned long long s1 = prof ? wall_clock64() : 0ull;
                 LaneState sr = T.st[v];
                 const int n_full = T.cnt[v];
                 const int n = n_full < e.max_legal ? n_full : e.max_legal;
-                WaveRng rng;
+                HalfRng rng;
                 rng.key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
                 rng.ctr = sr.ctr;
                 rng.refill();
                 if (n <= 0) {
-                    lane_advance(e, i, sr, rng, -1, sr.w, 0.0f, 0.0f, 0, l == 0);
+                    lane_advance(e, i, sr, rng, -1, sr.w, 0.0f, 0.0f, 0, lead);
                 } else {
                     const float* xv = xs + v * XS;   // V(s), then V(candidate k) at 1 + k
                     const float* vv = f.vbuf + (size_t)i * (f.cap + 1);
                     const float Tm = e.temperature;
                     const float u = unit_from(rng.at(0).x);   // lane_uniform: Philox at the lane's counter
                     const int pick =
-                        uniform(n + 1 <= XS
-                                    ? pick_action([&](int k) { return xv[1 + k] / Tm; }, n, e.greedy != 0, u)
-                                    : pick_action([&](int k) { return (1 + k < XS ? xv[1 + k] : vv[1 + k]) / Tm; }, n,
-                                                  e.greedy != 0, u));
+                        n + 1 <= XS
+                            ? pick_action_half([&](int k) { return xv[1 + k] / Tm; }, n, e.greedy != 0, u)
+                            : pick_action_half([&](int k) { return (1 + k < XS ? xv[1 + k] : vv[1 + k]) / Tm; }, n,
+                                               e.greedy != 0, u);
                     if (prof) tw[2] += wall_clock64() - s1;
                     uint32_t nb[8];
                     const int r = T.pre[v] + 1 + pick;
@@ -306,11 +309,12 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
                         load_packed(f.cand + ((size_t)i * f.cap + pick) * 8, nb);
                     }
                     const float va = 1 + pick < XS ? xv[1 + pick] : vv[1 + pick];
-                    lane_advance(e, i, sr, rng, pick, nb, xv[0], va, n_full, l == 0);
+                    lane_advance(e, i, sr, rng, pick, nb, xv[0], va, n_full, lead);
                 }
                 wave_sync();
-                if (l == 0) T.st[v] = sr;
+                if (lead) T.st[v] = sr;
                 if (prof) tw[3] += wall_clock64() - s1;
+                }
             }
             __syncthreads();
             tick(4);
