@@ -105,17 +105,27 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     gathered = [0, 0]
 
     def run(n):
-        left = n
+        # the gather of a harvest stays in flight while the next steps run and
+        # is waited at the next harvest (or the end of the run)
+        left, pending = n, None
+
+        def collect(p):
+            eps, recs = p.wait()
+            if rank == 0:
+                gathered[0] += eps
+                gathered[1] += recs
+
         while left > 0:
             k = min(harvest_every, left)
             eng.step(k)
             h = eng.harvest()
             if world > 1:
-                eps, recs = bdist.gather_episodes(h, dst=0)
-                if rank == 0:
-                    gathered[0] += eps
-                    gathered[1] += recs
+                if pending is not None:
+                    collect(pending)
+                pending = bdist.gather_episodes(h, dst=0, async_op=True)
             left -= k
+        if pending is not None:
+            collect(pending)
 
     run(warmup)
     eng.sync()

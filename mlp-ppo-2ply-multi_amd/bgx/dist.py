@@ -49,11 +49,29 @@ def _pad_rows(t, n, width, device):
     return out
 
 
-def gather_episodes(h, dst=0, keep=False):
+class PendingGather:
+    """An episode gather in flight (gather_episodes(..., async_op=True)):
+    wait() returns what the synchronous call returns. The buffers stay
+    referenced until then."""
+
+    def __init__(self, works, refs, result):
+        self._works, self._refs, self._result = works, refs, result
+
+    def wait(self):
+        for w in self._works:
+            w.wait()
+        self._works, self._refs = [], None
+        return self._result
+
+
+def gather_episodes(h, dst=0, keep=False, async_op=False):
     """Gather a Harvest (headers [n, 8], records [m, 24]) from every rank to `dst`.
 
     Returns (total_episodes, total_records) on dst ((0, 0) elsewhere); with
-    keep=True also the per-rank (headers, records) list on dst."""
+    keep=True also the per-rank (headers, records) list on dst. With
+    async_op=True the two data gathers are left in flight and a PendingGather
+    is returned (the counts exchange is still synchronous): the caller's next
+    engine steps overlap the transfer."""
     world, rank = dist.get_world_size(), dist.get_rank()
     dev = h.headers.device if dist.get_backend() == "nccl" else torch.device("cpu")
     cnt = torch.tensor([h.n_episodes, h.n_records], dtype=torch.int64, device=dev)
@@ -67,11 +85,13 @@ def gather_episodes(h, dst=0, keep=False):
     if rank == dst:
         hl = [torch.empty_like(hdr) for _ in range(world)]
         rl = [torch.empty_like(rec) for _ in range(world)]
-        dist.gather(hdr, hl, dst=dst)
-        dist.gather(rec, rl, dst=dst)
+        works = [dist.gather(hdr, hl, dst=dst, async_op=async_op), dist.gather(rec, rl, dst=dst, async_op=async_op)]
         parts = [(hl[r][: cnts[r][0]], rl[r][: cnts[r][1]]) for r in range(world)]
         tot = (sum(c[0] for c in cnts), sum(c[1] for c in cnts))
-        return (tot[0], tot[1], parts) if keep else tot
-    dist.gather(hdr, None, dst=dst)
-    dist.gather(rec, None, dst=dst)
-    return (0, 0, []) if keep else (0, 0)
+        result = (tot[0], tot[1], parts) if keep else tot
+        refs = (hdr, rec, hl, rl)
+    else:
+        works = [dist.gather(hdr, None, dst=dst, async_op=async_op), dist.gather(rec, None, dst=dst, async_op=async_op)]
+        result = (0, 0, []) if keep else (0, 0)
+        refs = (hdr, rec)
+    return PendingGather(works, refs, result) if async_op else result

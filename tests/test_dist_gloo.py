@@ -34,6 +34,12 @@ def _worker(rank, world, port, out):
     hdr[:, 0] = base
     rec = torch.full((3 * (rank + 1), 24), rank + 7, dtype=torch.int32)
     res = bdist.gather_episodes(Harvest(hdr, rec), dst=0, keep=True)
+    # the asynchronous form (bench.py overlaps it with the next steps) returns the same
+    pend = bdist.gather_episodes(Harvest(hdr, rec), dst=0, keep=True, async_op=True)
+    res_a = pend.wait()
+    assert res_a[:2] == res[:2]
+    for (h0, r0), (h1, r1) in zip(res[2], res_a[2]):
+        assert torch.equal(h0, h1) and torch.equal(r0, r1)
     if rank == 0:
         out.put(("w", got["b1"][0], got["b2"][0]))
         out.put(("tot", res[0], res[1], [int(p[0][0, 0]) for p in res[2]], [int(p[1][0, 0]) for p in res[2]]))
