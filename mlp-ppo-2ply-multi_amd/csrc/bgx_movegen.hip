@@ -58,18 +58,21 @@ __global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
 }
 
 // Tier 1 for large launches (the 2-ply replies), balanced: a workgroup of PW
-// waves owns a contiguous range of the jobs and its waves take the range's
-// next job from an LDS counter. With a static stride the launch lasts as long
-// as its unluckiest wave (67 jobs of very different cost each for the 344 k
-// reply jobs of a 4,096-lane K=4 step); here a wave that drew cheap jobs
-// takes more, and the 21 rolls of one candidate row stay on one CU (its L2).
-// The next job's board is loaded while the current job runs.
-constexpr int PW = 10;                                  // waves per workgroup (two per CU)
-constexpr int PF = Slice<S_T1>::F - 8;                  // frontier entries: 10 slices + the counter in 80 KB
+// waves owns the interleaved jobs b, b + G, ... and its waves take the next
+// one from an LDS counter. With a static per-wave stride the launch lasts as
+// long as its unluckiest wave (67 jobs of very different cost each for the
+// 344 k reply jobs of a 4,096-lane K=4 step); here a wave that drew cheap jobs
+// takes more. The next job's board is loaded while the current job runs.
+// PW waves per workgroup: 10 (two workgroups per CU, the default) or 5 (four)
+constexpr int PW = 10;
+constexpr int PF = Slice<S_T1>::F - 8;                  // frontier entries: PW slices + the counter fit
 constexpr int PSL = S_T1 * 8 + 2 * PF * 4 + 64 * 4;     // slice bytes
-static_assert(PW * PSL + 16 <= 80 * 1024, "two workgroups per CU");
+static_assert(PW * PSL + 16 <= 80 * 1024, "two 10-wave workgroups per CU");
+static_assert(5 * PSL + 16 <= 40 * 1024, "four 5-wave workgroups per CU");
 
-__global__ __launch_bounds__(64 * PW) void movegen_pool_kernel(MovegenArgs a) {
+template <int NWP>
+__global__ __launch_bounds__(64 * NWP) void movegen_pool_kernel(MovegenArgs a) {
+    constexpr int PW = NWP;
     __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
     __shared__ int next_job;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
@@ -272,13 +275,14 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         if (e != hipSuccess) return e;
     }
     // resident blocks per CU of each kernel (LDS, registers, 32 waves)
-    static int per_cu1 = 0, per_cub = 0, per_cuf = 0, per_cup = 0;
+    static int per_cu1 = 0, per_cub = 0, per_cuf = 0, per_cup = 0, per_cup5 = 0;
     if (!per_cu1) {
         auto occ = [](int& n, const void* k, int threads, int dflt) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n <= 0) n = dflt;
         };
         occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 64, 20);
-        occ(per_cup, (const void*)bgx::movegen_pool_kernel, 64 * bgx::PW, 2);
+        occ(per_cup, (const void*)bgx::movegen_pool_kernel<bgx::PW>, 64 * bgx::PW, 2);
+        occ(per_cup5, (const void*)bgx::movegen_pool_kernel<5>, 64 * 5, 4);
         occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
         occ(per_cuf, (const void*)bgx::movegen_few_kernel, bgx::NTH, 1);
     }
@@ -313,10 +317,14 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         hipLaunchKernelGGL(bgx::movegen_few_kernel, dim3(blocks), dim3(bgx::NTH), 0, stream, a);
     } else if (pool) {
         // balanced tier 1: 10-wave workgroups over contiguous job ranges
-        int blocks = n_cu * per_cup;
-        const int need = (a.n_jobs + bgx::PW - 1) / bgx::PW;
+        const int pw = poolm == 5 ? 5 : bgx::PW;   // BGX_MG_POOL=5: four 5-wave workgroups per CU
+        int blocks = n_cu * (pw == 5 ? per_cup5 : per_cup);
+        const int need = (a.n_jobs + pw - 1) / pw;
         if (!a.n_jobs_dev && need < blocks) blocks = need;
-        hipLaunchKernelGGL(bgx::movegen_pool_kernel, dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
+        if (pw == 5)
+            hipLaunchKernelGGL(bgx::movegen_pool_kernel<5>, dim3(blocks), dim3(64 * 5), 0, stream, a);
+        else
+            hipLaunchKernelGGL(bgx::movegen_pool_kernel<bgx::PW>, dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
     } else {
         int blocks = n_cu * per_cu1;
         if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;

@@ -34,8 +34,9 @@ def _run_movegen(ops, boards, player, dice, cap):
 
 # tier-1 kernel (large-launch "0" / 16-wave block "1") x heavy-doubles
 # hand-off to the block-cooperative tier 2 (off "0" / on "1") x the
-# large-launch kernel: balanced pool "1" (default) / strided per-wave "0"
-MG_MODES = [("0", "0", "1"), ("0", "0", "0"), ("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")]
+# large-launch kernel: balanced pool "1" (default, 10-wave workgroups) / "5"
+# (5-wave workgroups) / strided per-wave "0"
+MG_MODES = [("0", "0", "1"), ("0", "0", "0"), ("0", "0", "5"), ("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")]
 
 
 @pytest.mark.parametrize("few,coop,pool", MG_MODES)
