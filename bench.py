@@ -9,9 +9,17 @@ start from the reference's reset and play random-seeded self-play with the
 seeded xavier weights (tests/golden/weights_seed0.npz = torch.manual_seed(0)
 BackgammonPolicyNetwork()), T = 1.5 (ParameterManager version 1).
 
+Workload: 8,192 game lanes per GPU (weak scaling; N = 8 is configs[3]/[4]'s
+65,536 lanes sharded across 8 MI355X), 1-ply softmax select as the headline,
+with 2-ply K=4 (configs[4]) and K=all (configs[2]'s ~21 x C reply boards per
+decision) legs on the same lanes, and at N = 1 configs[1] (4,096 lanes) beside.
+
 N = 1:  python bench.py
-N > 1:  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
-            --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+N > 1:  python bench.py --gpus N      (starts N rank processes itself through
+            torch.distributed.run before anything touches a GPU), or as the
+            driver does: python -m torch.distributed.run --nnodes=1
+            --nproc-per-node N --master-addr 127.0.0.1 --master-port P
+            bench.py --gpus N
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -19,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -82,6 +92,17 @@ def max_over_ranks(x, world):
     t = torch.tensor([x], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_ranks(x, world):
+    """x from every rank, in rank order."""
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device())
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
 
 
 def sum_over_ranks(x, world):
@@ -155,11 +176,92 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     return el, d, tm, d_tm, gathered
 
 
-def cpu_baseline(seconds, threads):
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_worker(core, tasks, results):
+    """One pinned CPU-baseline process: runs the tasks it is sent, in order."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        os.sched_setaffinity(0, {core})   # one host core per process (BASELINE.md; main.py:86's 7 workers)
+    except (OSError, AttributeError):
+        pass
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc  # the bench's cpu_baseline leg (oracle = the CPU port)
-    r = orc.selfplay_bench(load_weights(), temperature=1.5, seed=0, n_threads=threads, seconds=seconds)
-    return r
+    w = load_weights()
+    while True:
+        t = tasks.get()
+        if t is None:
+            return
+        seed, ply, seconds = t
+        results.put(orc.selfplay_bench(w, temperature=1.5, seed=seed, n_threads=1, seconds=seconds, ply=ply))
+
+
+def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
+    """The CPU port of the worker loop (oracle/bgref.c, pinned by the golden
+    fixtures) as `procs` processes, each pinned to its own host core: one
+    1-ply round per seed (median of the per-round aggregates), then one 2-ply
+    K=4 round. Runs before this process touches the GPU."""
+    import multiprocessing as mp
+    cores = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
+    ctx = mp.get_context("spawn")
+    results = ctx.Queue()
+    tasks = [ctx.Queue() for _ in range(procs)]
+    ws = [ctx.Process(target=_cpu_worker, args=(cores[i % len(cores)], tasks[i], results), daemon=True)
+          for i in range(procs)]
+    for w in ws:
+        w.start()
+
+    def round_(seed, ply, seconds):
+        for i in range(procs):
+            tasks[i].put((1000 * seed + i, ply, seconds))
+        rs = [results.get(timeout=600) for _ in range(procs)]
+        return rs, max(r["elapsed"] for r in rs)
+
+    out = {}
+    try:
+        rates = []
+        for s in seeds:
+            rs, el = round_(s, 1, seconds_1ply)
+            rates.append(sum(r["steps"] for r in rs) / el)
+        out["1ply"] = {"rates": rates, "median": float(np.median(rates))}
+        if seconds_2ply > 0:
+            rs, el = round_(77, 2, seconds_2ply)
+            out["2ply"] = {"value": sum(r["steps"] for r in rs) / el,
+                           "decisions_per_s": sum(r["decisions"] for r in rs) / el, "elapsed": el}
+    finally:
+        for q in tasks:
+            q.put(None)
+        for w in ws:
+            w.join(timeout=60)
+    out["cores_used"] = min(procs, len(cores))
+    out["nproc"] = os.cpu_count()
+    out["affinity"] = len(cores)
+    out["cpu_model"] = _cpu_model()
+    return out
+
+
+def _pmc(leg, group, key):
+    """A per-launch PMC figure from the committed round profile
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc passes of this same bench workload), with its source."""
+    prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(prof) as f:
+            j = json.load(f)
+        v = j.get(leg, {}).get(group, {}).get(key)
+        src = f"profiles/pmc_traffic.json ({j.get('round', '?')}: {j.get('workload', '?')})"
+        return v, src
+    except (OSError, ValueError):
+        return None, None
 
 
 def roofline_fused(d, tm):
@@ -182,16 +284,10 @@ def roofline_fused(d, tm):
     m["frac"] = m["achieved"] / m["peak"]
     r = {kk: k[kk] for kk in ("bound", "achieved", "peak", "unit", "frac")}
     r["kernel"] = "bgx::fused_step_kernel (movegen + encode + MLP + select + env step, all steps of a launch)"
-    r["traffic"] = None
-    prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            with open(prof) as f:
-                per_step = json.load(f).get("1ply_fused", {}).get("fused", {}).get("hbm_bytes_per_step")
-                # PMC bytes per step (tools/profile_round.sh) x the steps of this bench's launches
-                r["traffic"] = per_step * k["steps_per_launch"] if per_step else None
-        except Exception:
-            r["traffic"] = None
+    # PMC bytes per step of the same workload x the steps of this bench's launches
+    per_step, src = _pmc("1ply_fused", "fused", "hbm_bytes_per_step")
+    r["traffic"] = per_step * k["steps_per_launch"] if per_step else None
+    r["traffic_source"] = src if per_step else None
     return r, {"fused_step": k, "fused_step_mfma": m}
 
 
@@ -219,18 +315,26 @@ def roofline_for(d, tm, leg):
         v["frac"] = v["achieved"] / v["peak"]
     dom = "movegen" if mg_ms >= mlp_ms else "mlp"
     r = {k: out[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")}
-    r["kernel"] = ({"1ply": "movegen launch = bgx::movegen_few_kernel + bgx::movegen_block_kernel",
-                    "2ply": "movegen launches = (few | pool) + bgx::movegen_block_kernel"}[leg]
+    r["kernel"] = (("movegen launch = bgx::movegen_few_kernel + bgx::movegen_block_kernel" if leg == "1ply" else
+                    "movegen launches = (few | pool) + bgx::movegen_block_kernel")
                    if dom == "movegen" else "bgx::mlp_kernel")
-    r["traffic"] = None
-    prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            with open(prof) as f:
-                r["traffic"] = json.load(f).get(leg, {}).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            r["traffic"] = None
+    r["traffic"], r["traffic_source"] = _pmc(leg, dom, "hbm_bytes_per_launch") if leg == "2ply_k4" else (None, None)
+    busy, bsrc = _pmc(leg, dom, "valu_busy") if leg == "2ply_k4" else (None, None)
+    if busy is not None:
+        r["valu_busy"], r["valu_busy_source"] = busy, bsrc
     return r, out
+
+
+def spawn_ranks(n):
+    """bench.py --gpus N without a torch.distributed launcher: start the N
+    rank processes through torch.distributed.run from this process, which
+    has not touched a GPU, and exit with their status."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -238,17 +342,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=300)
-    ap.add_argument("--lanes", type=int, default=4096, help="lanes per GPU (configs[1]: 4096)")
+    ap.add_argument("--lanes", type=int, default=8192,
+                    help="lanes per GPU (8,192: configs[3]/[4]'s 65,536 lanes over 8 GPUs)")
     ap.add_argument("--ply", type=int, default=1)
     ap.add_argument("--k-top", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--harvest-every", type=int, default=300,
-                    help="steps per bgx_step launch between harvests (<= ring - max_steps = 340)")
-    ap.add_argument("--two-ply-steps", type=int, default=100, help="extra 2-ply (K=4) measurement; 0 = skip")
+                    help="steps per bgx_step launch between harvests (<= ring - max_steps)")
+    ap.add_argument("--two-ply-steps", type=int, default=100, help="2-ply K=4 leg (configs[4]); 0 = skip")
     ap.add_argument("--kall-steps", type=int, default=20,
-                    help="extra 2-ply K=all measurement (configs[2]: ~21 x C reply boards per decision); 0 = skip")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=7, help="mirrors src/main.py:86 (7 workers)")
+                    help="2-ply K=all leg (configs[2]: ~21 x C reply boards per decision); 0 = skip")
+    ap.add_argument("--config1-steps", type=int, default=300,
+                    help="N = 1: configs[1] (4,096 lanes, 1-ply) beside the headline; 0 = skip")
+    ap.add_argument("--cpu-procs", type=int, default=7, help="pinned CPU-port processes (src/main.py:86: 7 workers)")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="per 1-ply round (one round per seed)")
+    ap.add_argument("--cpu-seeds", type=int, default=5, help="seeds 0..n-1, median reported")
+    ap.add_argument("--cpu-2ply-seconds", type=float, default=4.0, help="2-ply CPU round (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true",
                     help="1-ply: one launch per phase and step instead of the fused persistent step kernel")
@@ -256,79 +365,87 @@ def main():
                     help="length of the event-timed pass that feeds roofline (2-ply: min(this, 50))")
     args = ap.parse_args()
 
-    world, rank, local = init_dist()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
 
-    el, d, tm, d_tm, gathered = run_engine(args, world, rank, args.ply, args.k_top, args.lanes, args.steps,
-                                           args.warmup, args.harvest_every, timing=True,
-                                           timing_steps=min(args.steps, args.timing_steps))
-    el = max_over_ranks(el, world)
-    total_steps = sum_over_ranks(d["env_steps"], world)
-    value = total_steps / el
-    roof, kernels = roofline_for(d_tm, tm, f"{args.ply}ply")
-
-    extra = {}
-    if args.two_ply_steps > 0 and args.ply == 1:
-        el2, d2, tm2, d2_tm, _ = run_engine(args, world, rank, 2, 4, args.lanes, args.two_ply_steps, 20,
-                                            args.harvest_every, timing=True,
-                                            timing_steps=min(args.two_ply_steps, args.timing_steps, 50))
-        el2 = max_over_ranks(el2, world)
-        tot2 = sum_over_ranks(d2["env_steps"], world)
-        r2, k2 = roofline_for(d2_tm, tm2, "2ply")
-        extra["two_ply_k4"] = {"value": tot2 / el2, "unit": "env_steps/s", "steps": args.two_ply_steps,
-                               "ms_per_step": el2 / args.two_ply_steps * 1e3,
-                               "value_rows_per_s": sum_over_ranks(d2["value_rows"], world) / el2,
-                               "movegen_jobs_per_s": sum_over_ranks(d2["movegen_jobs"], world) / el2,
-                               "roofline": r2, "kernels": k2}
-
-    if args.kall_steps > 0 and args.ply == 1:
-        el3, d3, tm3, d3_tm, _ = run_engine(args, world, rank, 2, 0, args.lanes, args.kall_steps, 5,
-                                            args.harvest_every, timing=True,
-                                            timing_steps=min(args.kall_steps, args.timing_steps, 10))
-        el3 = max_over_ranks(el3, world)
-        tot3 = sum_over_ranks(d3["env_steps"], world)
-        r3, k3 = roofline_for(d3_tm, tm3, "2ply")
-        r3["traffic"] = None   # the PMC passes cover the K=4 leg
-        extra["two_ply_kall"] = {"value": tot3 / el3, "unit": "env_steps/s", "steps": args.kall_steps,
-                                 "ms_per_step": el3 / args.kall_steps * 1e3,
-                                 "value_rows_per_s": sum_over_ranks(d3["value_rows"], world) / el3,
-                                 "movegen_jobs_per_s": sum_over_ranks(d3["movegen_jobs"], world) / el3,
-                                 "reply_boards_per_decision": (d3["value_rows"] - 2 * d3["env_steps"])
-                                 / max(1, d3["decisions"]),
-                                 "roofline": r3, "kernels": k3}
-
+    # the CPU baseline first, on rank 0 at N = 1, before this process touches the GPU
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        r = cpu_baseline(args.cpu_seconds, args.cpu_threads)
-        cpu = {"value": r["steps"] / r["elapsed"], "unit": "env_steps/s", "cores": r["threads"], "kind": "port",
-               "sample": f"{r['threads']} host threads x {r['elapsed']:.1f} s of 1-ply self-play with the CPU "
-                         f"oracle port (oracle/bgref.c; same weights, T=1.5): {r['steps']} env steps, "
-                         f"{r['episodes']} episodes; reference Python 7-worker path measured 2052 env steps/s "
-                         f"in the survey container (BASELINE.md)"}
+    if world_env == 1 and not args.no_cpu_baseline:
+        r = cpu_baseline(args.cpu_procs, args.cpu_seconds, list(range(args.cpu_seeds)), args.cpu_2ply_seconds)
+        cpu = {"value": r["1ply"]["median"], "unit": "env_steps/s", "cores": r["cores_used"], "kind": "port",
+               "sample": (f"{args.cpu_procs} processes, each pinned to one host core, x {args.cpu_seconds:.0f} s "
+                          f"of 1-ply self-play per seed (seeds 0-{args.cpu_seeds - 1}, median of "
+                          f"{[round(x) for x in r['1ply']['rates']]}) with the CPU port of the worker loop "
+                          f"(oracle/bgref.c; same weights, T=1.5); host: {r['cpu_model']}, nproc {r['nproc']}, "
+                          f"{r['affinity']} cores in this process's affinity mask; the reference's own Python "
+                          f"7-worker path measured 2,052 env steps/s in the survey container (BASELINE.md)"),
+               "cpu_model": r["cpu_model"], "nproc": r["nproc"]}
+        if "2ply" in r:
+            cpu["two_ply_k4"] = {"value": r["2ply"]["value"], "unit": "env_steps/s",
+                                 "decisions_per_s": r["2ply"]["decisions_per_s"],
+                                 "sample": f"{args.cpu_procs} pinned processes x {r['2ply']['elapsed']:.1f} s of "
+                                           "2-ply K=4 self-play (exact mode, fp32) with the same CPU port; the "
+                                           "reference's Python 2-ply takes 205 ms per decision (BASELINE.md)"}
 
-    sums = {k: sum_over_ranks(d[k], world) for k in ("decisions", "episodes", "value_rows", "fallback_jobs")}
+    world, rank, local = init_dist()
+
+    def leg(ply, k_top, lanes, steps, warmup, timing_steps, name):
+        el_, d_, tm_, dtm_, gathered_ = run_engine(args, world, rank, ply, k_top, lanes, steps, warmup,
+                                                   args.harvest_every, timing=True, timing_steps=timing_steps)
+        el_ = max_over_ranks(el_, world)
+        per_rank = [int(x) for x in all_ranks(d_["env_steps"], world)]
+        roof_, kern_ = roofline_for(dtm_, tm_, name)
+        out_ = {"value": sum(per_rank) / el_, "unit": "env_steps/s", "steps": steps, "lanes_per_gpu": lanes,
+                "ms_per_step": el_ / steps * 1e3, "env_steps_per_rank": per_rank,
+                "decisions_per_s": sum_over_ranks(d_["decisions"], world) / el_,
+                "episodes_per_s": sum_over_ranks(d_["episodes"], world) / el_,
+                "value_rows_per_s": sum_over_ranks(d_["value_rows"], world) / el_,
+                "movegen_jobs_per_s": sum_over_ranks(d_["movegen_jobs"], world) / el_,
+                "fallback_jobs": int(sum_over_ranks(d_["fallback_jobs"], world)),
+                "roofline": roof_, "kernels": kern_}
+        if world > 1:
+            out_["gathered_episodes"], out_["gathered_records"] = gathered_
+        return out_, d_
+
+    head, d = leg(args.ply, args.k_top, args.lanes, args.steps, args.warmup, min(args.steps, args.timing_steps),
+                  "1ply" if args.ply == 1 else ("2ply_k4" if args.k_top == 4 else "2ply_kall"))
+    extra = {}
+    if args.ply == 1 and args.two_ply_steps > 0:
+        extra["two_ply_k4"], _ = leg(2, 4, args.lanes, args.two_ply_steps, 20,
+                                     min(args.two_ply_steps, args.timing_steps, 50), "2ply_k4")
+    if args.ply == 1 and args.kall_steps > 0:
+        extra["two_ply_kall"], d3 = leg(2, 0, args.lanes, args.kall_steps, 5,
+                                        min(args.kall_steps, args.timing_steps, 10), "2ply_kall")
+        extra["two_ply_kall"]["reply_boards_per_decision"] = \
+            (d3["value_rows"] - 2 * d3["env_steps"]) / max(1, d3["decisions"])
+    if args.ply == 1 and world == 1 and args.config1_steps > 0 and args.lanes != 4096:
+        c1, _ = leg(1, 4, 4096, args.config1_steps, 100, min(args.config1_steps, args.timing_steps), "1ply")
+        extra["configs1_4096_lanes"] = {k: c1[k] for k in ("value", "unit", "steps", "ms_per_step", "roofline")}
+
     if rank == 0:
         line = {
-            "metric": METRIC, "value": value, "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "metric": METRIC, "value": head["value"], "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8 game state + fp16x2-split MFMA (fp32 acc)",
             "data": "synthetic: random-seeded self-play from the reference reset, seeded xavier weights",
-            "config": {"workload": f"{args.lanes} game lanes per GPU, {args.ply}-ply softmax select"
-                                   + (" (configs[1])" if args.ply == 1 and args.lanes == 4096 else ""),
+            "config": {"workload": (f"{args.lanes} game lanes per GPU ({args.lanes * world} total), "
+                                    f"{args.ply}-ply" + (" softmax select" if args.ply == 1 else
+                                                        f" K={args.k_top or 'all'}")
+                                    + (" (configs[3]/[4] lane shard: 65,536 lanes at N=8)"
+                                       if args.lanes == 8192 else "")),
                        "lanes_per_gpu": args.lanes, "lanes_total": args.lanes * world, "ply": args.ply,
                        "harvest_every": args.harvest_every,
                        "engine": "fused step kernel" if args.ply == 1 and not args.no_fused else "phased launches",
-                       "parallelism": f"lanes sharded x{world}, "
-                       "RCCL episode gather" if world > 1 else "single GPU"},
-            "decisions_per_s": sums["decisions"] / el,
-            "episodes_per_s": sums["episodes"] / el,
-            "value_rows_per_s": sums["value_rows"] / el,
-            "fallback_jobs": int(sums["fallback_jobs"]),
-            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu,
+                       "parallelism": (f"lanes sharded x{world}, RCCL episode gather to rank 0 "
+                                       f"({BACKEND})" if world > 1 else "single GPU")},
+            "world_size": world, "env_steps_per_rank": head["env_steps_per_rank"],
+            "decisions_per_s": head["decisions_per_s"], "episodes_per_s": head["episodes_per_s"],
+            "value_rows_per_s": head["value_rows_per_s"], "fallback_jobs": head["fallback_jobs"],
+            "roofline": head["roofline"], "kernels": head["kernels"], "cpu_baseline": cpu,
         }
         if world > 1:
-            line["gathered_episodes"] = gathered[0]
+            line["gathered_episodes"], line["gathered_records"] = head["gathered_episodes"], head["gathered_records"]
         line.update(extra)
         print(json.dumps(line))
     if world > 1:

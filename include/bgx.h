@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 4
+#define BGX_ABI_VERSION 5
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -96,10 +96,13 @@ typedef struct bgx_config {
     int ply;                /* 1 = worker.py:78-174 softmax(V/T); 2 = two_ply.py scoring */
     int k_top;              /* 2-ply candidates: 4 (reference, two_ply.py:67-70) or 0 = all */
     float alpha, beta;      /* 2-ply score = alpha*S - beta*W (two_ply.py:44-50): 1.0, 0.9 */
-    int max_steps;          /* MAX_TIMESTEPS (config/configuration.py:4): 300 */
-    int max_legal;          /* BackgammonEnv max_legal_moves (backgammon_env.py:35): 500 */
-    int ring;               /* experience ring slots per lane (>= max_steps + steps between harvests) */
-    int ep_cap;             /* finished-episode headers held between harvests */
+    int max_steps;          /* MAX_TIMESTEPS (config/configuration.py:4): 300 (at most 511) */
+    int max_legal;          /* BackgammonEnv max_legal_moves (backgammon_env.py:35): 500; at most 512
+                               (phased engine) or 2048 (fused 1-ply engine) */
+    int ring;               /* experience ring slots per lane (>= max_steps + steps between harvests;
+                               rounded up to a power of two; default 1024) */
+    int ep_cap;             /* finished-episode headers held between harvests (0 = derived: every
+                               episode that can finish in ring - max_steps steps) */
     int cand_per_lane;      /* average candidate rows reserved per lane (1-ply buffer) */
     int reply_per_lane;     /* average 2-ply reply rows reserved per lane */
     int greedy;             /* 1: argmax of the scores instead of sampling (play_versus_ai.py:188-195,
@@ -125,6 +128,15 @@ int bgx_engine_destroy(bgx_engine* e);
 int bgx_set_weights(bgx_engine* e, const float* h_W1, const float* h_b1, const float* h_w2,
                     const float* h_b2, float temperature, uint64_t version);
 
+/* Test hook for parity replays: scripted dice. h_dice (host) holds, per lane,
+ * per_lane single-die draws (1..6) that replace np.random.randint(1, 7)
+ * (backgammon_env.py:310-311): every roll takes the lane's next two, starting
+ * with BackgammonEnv.reset's starter and first rolls (backgammon_env.py:92-128).
+ * Needs cfg.greedy (no sampling uniform is drawn); every lane restarts from
+ * the reset. Reading past a lane's draws raises BGX_E_CAPACITY at the next
+ * bgx_sync / bgx_harvest (the roll is then 1-2). */
+int bgx_engine_set_dice(bgx_engine* e, const uint8_t* h_dice, int per_lane);
+
 /* Advance every lane by n_steps env steps (one BackgammonEnv.step each,
  * passes included; finished games are recorded and the lane restarts). */
 int bgx_step(bgx_engine* e, int n_steps, void* stream);
@@ -133,13 +145,20 @@ int bgx_sync(bgx_engine* e);
 
 /* Finished episodes since the last harvest (Episode/Experience,
  * environments/episode.py:5-84). Both arrays are DEVICE memory owned by the
- * engine, valid until the next bgx_harvest/bgx_step:
- *   headers [n_episodes][8] u32: global lane, episode no., first record,
- *     n_records, env steps, win_type | winner << 8 | flags << 16
- *   records [n_records][24] u32: before board (packed, 8 u32), after board
- *     (packed), V(s) f32, V(a) f32, reward f32, action | n_moves << 16,
- *     dice0 | dice1 << 8 | done << 16 | close_out << 17 | prime << 18 |
- *     mover << 19 | win_type << 20, episode no., step, global lane.
+ * engine, valid until the next bgx_harvest/bgx_step; each episode's records
+ * are contiguous, in header order:
+ *   headers [n_episodes][16] u32: global lane, episode no., first record,
+ *     n_records, env steps, win_type | winner << 8 | flags << 16, the final
+ *     board (packed words 0..6), 0, 0, 0
+ *   records [n_records][12] u32 (48 B): the board before the move (packed
+ *     words 0..6; the indicator = the mover), V(s) f32, V(a) f32, reward f32,
+ *     action | n_moves << 11 | step << 23 (n_moves saturates at 4095),
+ *     dice0 | dice1 << 3 | done << 6 | close_out << 7 | prime << 8 |
+ *     mover << 9 | win_type << 10.
+ * The board after record k's move (Experience.next_observation) is record
+ * k+1's before-board (passes move no checker), and for an episode's last
+ * record the header's final board; its indicator is the mover at a terminal
+ * step (the winner), else the other player (backgammon_env.py:196-218).
  * Packed board: u32[8]: P1 point nibbles [0..2], P2 [3..5], w[6] = bar1 |
  * bar2 << 4 | off1 << 8 | off2 << 12 | indicator player << 16.
  * Synchronizes the engine stream. */

@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("BGX_LIB", os.path.join(_HERE, "libbgx.so"))
 c_int, c_float, c_double, c_u64, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                              ctypes.c_uint64, ctypes.c_void_p)
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class BgxError(RuntimeError):
@@ -64,6 +64,7 @@ SIGNATURES = {
     "bgx_engine_create": (c_int, [c_int, ctypes.POINTER(Config), ctypes.POINTER(c_void_p)]),
     "bgx_engine_destroy": (c_int, [c_void_p]),
     "bgx_set_weights": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_u64]),
+    "bgx_engine_set_dice": (c_int, [c_void_p, c_void_p, c_int]),
     "bgx_step": (c_int, [c_void_p, c_int, c_void_p]),
     "bgx_sync": (c_int, [c_void_p]),
     "bgx_harvest": (c_int, [c_void_p, ctypes.POINTER(HarvestInfo), c_void_p]),

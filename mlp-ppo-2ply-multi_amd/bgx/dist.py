@@ -6,8 +6,9 @@ src/multi/experience_queue.py:5-13, src/multi/parameter_manager.py:79-91).
 Here every rank runs its own Engine over a disjoint block of global lane ids
 (so results do not depend on the GPU count) and the only collectives are:
   * broadcast_weights  — the 102,404-byte fp32 state on each version bump;
-  * gather_episodes    — compact headers/records of finished episodes to the
-                         trainer rank (RCCL point-to-point over xGMI).
+  * gather_episodes    — compact headers (64 B) / records (48 B) of finished
+                         episodes to the trainer rank (RCCL point-to-point
+                         over xGMI, exact sizes, no padding).
 There is no per-step exchange.
 """
 from __future__ import annotations
@@ -15,6 +16,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 import torch.distributed as dist
+
+from .records import EP_WORDS, REC_WORDS
 
 KEYS = ("W1", "b1", "w2", "b2")
 
@@ -42,13 +45,6 @@ def broadcast_weights(w, src=0, device=None):
     return out
 
 
-def _pad_rows(t, n, width, device):
-    out = torch.zeros((n, width), dtype=torch.int32, device=device)
-    if t.shape[0]:
-        out[: t.shape[0]] = t
-    return out
-
-
 class PendingGather:
     """An episode gather in flight (gather_episodes(..., async_op=True)):
     wait() returns what the synchronous call returns. The buffers stay
@@ -65,33 +61,57 @@ class PendingGather:
 
 
 def gather_episodes(h, dst=0, keep=False, async_op=False):
-    """Gather a Harvest (headers [n, 8], records [m, 24]) from every rank to `dst`.
+    """Gather a Harvest (headers [n, 16], records [m, 12]) from every rank to `dst`.
 
+    Two steps: the per-rank counts go to dst (one 16-byte gather), then each
+    rank with episodes sends exactly its headers and records to dst by
+    point-to-point send / recv (RCCL over xGMI with the nccl backend; no
+    padding to the largest rank, nothing sent by a rank with no episodes).
     Returns (total_episodes, total_records) on dst ((0, 0) elsewhere); with
     keep=True also the per-rank (headers, records) list on dst. With
-    async_op=True the two data gathers are left in flight and a PendingGather
-    is returned (the counts exchange is still synchronous): the caller's next
-    engine steps overlap the transfer."""
+    async_op=True the point-to-point transfers are left in flight and a
+    PendingGather is returned (the counts step is synchronous): the caller's
+    next engine steps overlap the transfer."""
     world, rank = dist.get_world_size(), dist.get_rank()
-    dev = h.headers.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    nccl = dist.get_backend() == "nccl"
+    dev = h.headers.device if nccl else torch.device("cpu")
     cnt = torch.tensor([h.n_episodes, h.n_records], dtype=torch.int64, device=dev)
-    cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt)
-    cnts = [tuple(int(x) for x in c.tolist()) for c in cnts]
-    me = max(c[0] for c in cnts)
-    mr = max(c[1] for c in cnts)
-    hdr = _pad_rows(h.headers.to(dev), max(me, 1), 8, dev)
-    rec = _pad_rows(h.records.to(dev), max(mr, 1), 24, dev)
     if rank == dst:
-        hl = [torch.empty_like(hdr) for _ in range(world)]
-        rl = [torch.empty_like(rec) for _ in range(world)]
-        works = [dist.gather(hdr, hl, dst=dst, async_op=async_op), dist.gather(rec, rl, dst=dst, async_op=async_op)]
-        parts = [(hl[r][: cnts[r][0]], rl[r][: cnts[r][1]]) for r in range(world)]
+        cnts_t = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.gather(cnt, cnts_t, dst=dst)
+        cnts = [tuple(int(x) for x in c.tolist()) for c in cnts_t]
+    else:
+        dist.gather(cnt, None, dst=dst)
+        cnts = None
+    ops, refs = [], []
+    if rank == dst:
+        parts = []
+        for r in range(world):
+            ne, nr = cnts[r]
+            if r == dst:
+                parts.append((h.headers.to(dev), h.records.to(dev)))
+                continue
+            hb = torch.empty((ne, EP_WORDS), dtype=torch.int32, device=dev)
+            rb = torch.empty((nr, REC_WORDS), dtype=torch.int32, device=dev)
+            if ne:
+                ops.append(dist.P2POp(dist.irecv, hb, r))
+            if nr:
+                ops.append(dist.P2POp(dist.irecv, rb, r))
+            parts.append((hb, rb))
+            refs += [hb, rb]
         tot = (sum(c[0] for c in cnts), sum(c[1] for c in cnts))
         result = (tot[0], tot[1], parts) if keep else tot
-        refs = (hdr, rec, hl, rl)
     else:
-        works = [dist.gather(hdr, None, dst=dst, async_op=async_op), dist.gather(rec, None, dst=dst, async_op=async_op)]
+        hs, rs = h.headers.to(dev).contiguous(), h.records.to(dev).contiguous()
+        if h.n_episodes:
+            ops.append(dist.P2POp(dist.isend, hs, dst))
+        if h.n_records:
+            ops.append(dist.P2POp(dist.isend, rs, dst))
+        refs += [hs, rs]
         result = (0, 0, []) if keep else (0, 0)
-        refs = (hdr, rec)
-    return PendingGather(works, refs, result) if async_op else result
+    works = dist.batch_isend_irecv(ops) if ops else []
+    if async_op:
+        return PendingGather(works, refs, result)
+    for w in works:
+        w.wait()
+    return result

@@ -13,16 +13,13 @@ import torch
 
 from ._lib import Config, HarvestInfo, Stats, check, lib, require_cuda, stream_handle
 from .ops import weights_from
-
-REC_WORDS = 24
-EP_WORDS = 8
-WIN_TYPES = {0: None, 1: "regular", 2: "gammon", 3: "backgammon"}
+from .records import EP_WORDS, REC_WORDS, WIN_TYPES  # noqa: F401  (wire format, include/bgx.h)
 
 
 @dataclass
 class Harvest:
-    """Finished episodes: headers int32 [n, 8] and records int32 [m, 24] on the
-    engine's device (layouts in include/bgx.h, bgx_harvest)."""
+    """Finished episodes: headers int32 [n, 16] and records int32 [m, 12] on the
+    engine's device (layouts in include/bgx.h, bgx_harvest; bgx/records.py)."""
     headers: torch.Tensor
     records: torch.Tensor
 
@@ -37,7 +34,7 @@ class Harvest:
 
 class Engine:
     def __init__(self, lanes=4096, seed=0, ply=1, k_top=4, device=None, lane_base=0, alpha=1.0,
-                 beta=0.9, max_steps=300, max_legal=500, ring=640, ep_cap=0, cand_per_lane=256,
+                 beta=0.9, max_steps=300, max_legal=500, ring=1024, ep_cap=0, cand_per_lane=256,
                  reply_per_lane=0, greedy=False, fused=True, reply_sample=0):
         require_cuda()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
@@ -83,6 +80,16 @@ class Engine:
         check(lib().bgx_set_weights(self._h, fp(W1), fp(b1), fp(w2), fp(b2), float(temperature),
                                     int(version)), "bgx_set_weights")
         self.version, self.temperature = int(version), float(temperature)
+
+    def set_dice(self, dice):
+        """Test hook (bgx_engine_set_dice): scripted single-die draws, uint8
+        [lanes, k] in 1..6, two per roll, replacing np.random.randint(1, 7)
+        (backgammon_env.py:310-311); needs greedy=True. Every lane restarts
+        from the reset with its own draws."""
+        import numpy as np
+        d = np.ascontiguousarray(np.asarray(dice, dtype=np.uint8).reshape(self.lanes, -1))
+        check(lib().bgx_engine_set_dice(self._h, d.ctypes.data_as(ctypes.c_void_p), int(d.shape[1])),
+              "bgx_engine_set_dice")
 
     def step(self, n=1, stream=None):
         """Advance every lane by n env steps (asynchronous on the stream)."""

@@ -15,36 +15,35 @@ import numpy as np
 import torch
 
 from . import ops
-from .engine import WIN_TYPES, Harvest
+from . import records as records_np
+from .engine import Harvest
+from .records import REC_WORDS, WIN_TYPES
 
 
-def decode_records(records: torch.Tensor):
-    """records int32 [m, 24] (device) -> dict of host numpy arrays, with the
-    198-d observations encoded on the device."""
+def decode_records(headers, records: torch.Tensor):
+    """Harvested episodes -> dict of host numpy arrays: the record fields
+    (bgx/records.py) plus the boards before / after every move (u8 [m, 52])
+    and the 198-d observations, encoded on the device (bgx_encode).
+    headers: uint32/int32 [n, 16] (host or device); records int32 [m, 12]
+    (device), each episode's records contiguous in header order."""
+    hdr = headers.cpu().numpy() if isinstance(headers, torch.Tensor) else np.asarray(headers)
     m = records.shape[0]
     if m == 0:
         z = np.zeros((0, 198), np.float32)
-        return dict(obs=z, next_obs=z, v_s=np.zeros(0, np.float32), v_a=np.zeros(0, np.float32),
-                    reward=np.zeros(0, np.float32), done=np.zeros(0, bool), action=np.zeros(0, np.int32),
-                    n_moves=np.zeros(0, np.int32), dice=np.zeros((0, 2), np.int32),
-                    close_out=np.zeros(0, bool), prime=np.zeros(0, bool), mover=np.zeros(0, np.int32),
-                    win_type=np.zeros(0, np.int32), before=np.zeros((0, 52), np.uint8),
-                    after=np.zeros((0, 52), np.uint8), step=np.zeros(0, np.int32))
-    before, after = records[:, 0:8].contiguous(), records[:, 8:16].contiguous()
-    b8, a8 = ops.unpack(before), ops.unpack(after)
-    obs = ops.encode(b8, ops.packed_player(before))
-    nxt = ops.encode(a8, ops.packed_player(after))
-    tail = records[:, 16:24].cpu().numpy()
-    f = tail[:, 0:3].copy().view(np.float32)
-    w3, w4 = tail[:, 3].astype(np.uint32), tail[:, 4].astype(np.uint32)
-    return dict(
-        obs=obs.cpu().numpy(), next_obs=nxt.cpu().numpy(), v_s=f[:, 0], v_a=f[:, 1], reward=f[:, 2],
-        action=(w3 & 0xFFFF).astype(np.int32), n_moves=(w3 >> 16).astype(np.int32),
-        dice=np.stack([(w4 & 0xFF), (w4 >> 8) & 0xFF], 1).astype(np.int32),
-        done=((w4 >> 16) & 1).astype(bool), close_out=((w4 >> 17) & 1).astype(bool),
-        prime=((w4 >> 18) & 1).astype(bool), mover=((w4 >> 19) & 1).astype(np.int32),
-        win_type=((w4 >> 20) & 7).astype(np.int32), before=b8.cpu().numpy(), after=a8.cpu().numpy(),
-        step=tail[:, 6].astype(np.int32))
+        out = {k: v for k, v in records_np.fields(np.zeros((0, REC_WORDS), np.uint32)).items()}
+        out.update(obs=z, next_obs=z, before=np.zeros((0, 52), np.uint8), after=np.zeros((0, 52), np.uint8))
+        return out
+    rec = records.cpu().numpy()
+    before, after = records_np.packed_before_after(hdr, rec)
+    dev = records.device
+    b_t = torch.from_numpy(before.view(np.int32)).to(dev)
+    a_t = torch.from_numpy(after.view(np.int32)).to(dev)
+    b8, a8 = ops.unpack(b_t), ops.unpack(a_t)
+    out = records_np.fields(rec)
+    out.update(obs=ops.encode(b8, ops.packed_player(b_t)).cpu().numpy(),
+               next_obs=ops.encode(a8, ops.packed_player(a_t)).cpu().numpy(),
+               before=b8.cpu().numpy(), after=a8.cpu().numpy())
+    return out
 
 
 def to_episodes(h: Harvest, episode_cls, experience_cls, player_enum):
@@ -54,11 +53,11 @@ def to_episodes(h: Harvest, episode_cls, experience_cls, player_enum):
 
 
 def episodes_from_arrays(hdr, records, episode_cls, experience_cls, player_enum):
-    """hdr uint32 [n, 8] (host), records int32 [m, 24] (device) -> Episodes.
+    """hdr uint32 [n, 16] (host), records int32 [m, 12] (device) -> Episodes.
     Field types follow Episode.to_numpy() (episode.py:22-46): observation
     np.float32[198] views, state values Python floats, reward a 0-d np.float32
     array, done bool."""
-    d = decode_records(records)
+    d = decode_records(hdr, records)
     obs, nxt = d["obs"], d["next_obs"]
     v_s, v_a, done = d["v_s"].tolist(), d["v_a"].tolist(), d["done"].tolist()
     rew = d["reward"].astype(np.float32).reshape(-1, 1)

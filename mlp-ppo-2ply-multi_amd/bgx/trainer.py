@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
-from .engine import WIN_TYPES
+from .records import WIN_TYPES
 from .net import BackgammonPolicyNetwork
 
 LEARNING_RATE = 1e-3          # config/configuration.py:17
@@ -52,9 +52,10 @@ class DeviceTrainer:
         rec = torch.as_tensor(records).to(self.device)
         if rec.dtype != torch.int32:
             rec = rec.view(torch.int32) if rec.dtype == torch.uint32 else rec.to(torch.int32)
-        before = rec[:, 0:8].contiguous()
+        before = torch.zeros((rec.shape[0], 8), dtype=torch.int32, device=self.device)
+        before[:, :7] = rec[:, :7]   # the board before the move, the mover's indicator (bgx/records.py)
         obs = ops.encode(ops.unpack(before), ops.packed_player(before))
-        rewards = rec[:, 18].contiguous().view(torch.float32)
+        rewards = rec[:, 9].contiguous().view(torch.float32)
         hdr = np.asarray(torch.as_tensor(headers).cpu().numpy()).astype(np.uint32)
         lens = hdr[:, 3].astype(np.int64).tolist()
         wins = [WIN_TYPES[int(w) & 0xFF] for w in (hdr[:, 5] & 0xFF).tolist()]
@@ -78,7 +79,7 @@ class DeviceTrainer:
         return self._update(*self._from_episodes(episodes))
 
     def update_records(self, headers, records):
-        """The same update from compact records (headers [n, 8], records [m, 24],
+        """The same update from compact records (headers [n, 16], records [m, 12],
         each episode's records contiguous in header order); any n >= 1."""
         return self._update(*self._from_records(headers, records))
 

@@ -11,6 +11,8 @@
 #include <cstring>
 #include <string>
 #include <cstdlib>
+#include <exception>
+#include <new>
 #include <vector>
 
 #include "bgx.h"
@@ -162,6 +164,11 @@ struct bgx_engine {
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;   // pairs: movegen, mlp
+    // test / development hooks, read once at create: BGX_MG_TEST_TIER (fused
+    // movegen tiers), BGX_FUSED_PROF (phase clocks, printed at destroy)
+    int force_tier = 0;
+    bool prof_enabled = false;
+    uint8_t* dice_tab = nullptr;  // bgx_engine_set_dice
     std::vector<int> ev_kind;
     double ms_mg = 0, ms_mlp = 0;
     int n_mg = 0, n_mlp = 0;
@@ -176,6 +183,34 @@ namespace {
 constexpr int C_EP = 3, C_ERR = 4, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
 }
 
+static int check_flags(bgx_engine* e) {
+    unsigned f = 0;
+    HIP_TRY(hipMemcpy(&f, e->ctr + C_ERR, 4, hipMemcpyDeviceToHost));
+    if (f) {
+        HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
+        return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
+                    "workspace, 8 experience ring, 16 episode list, 32 scripted dice)", f);
+    }
+    return BGX_OK;
+}
+
+
+// Every int entry point runs inside guarded(): a C++ exception (std::bad_alloc
+// from a host vector, ...) becomes an error code and bgx_last_error(), never an
+// unwind across the C boundary.
+template <typename F>
+static int guarded(const char* what, F&& body) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return fail(BGX_E_CAPACITY, "%s: host allocation failed", what);
+    } catch (const std::exception& ex) {
+        return fail(BGX_E_STATE, "%s: %s", what, ex.what());
+    } catch (...) {
+        return fail(BGX_E_STATE, "%s: unexpected C++ exception", what);
+    }
+}
+
 extern "C" {
 
 int bgx_abi_version(void) { return BGX_ABI_VERSION; }
@@ -183,216 +218,236 @@ const char* bgx_last_error(void) { return g_err.c_str(); }
 
 int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t* d_dice, int n,
                 uint8_t* d_out_boards, int32_t* d_out_count, int cap, void* stream) {
-    if (n < 0 || cap < 0) return fail(BGX_E_ARG, "bgx_movegen: n=%d cap=%d", n, cap);
-    if (n == 0) return BGX_OK;
-    if (!d_boards || !d_player || !d_dice || !d_out_count || (cap > 0 && !d_out_boards))
-        return fail(BGX_E_ARG, "bgx_movegen: null pointer");
-    // per-call scratch for the overflow path (kept across calls)
-    static unsigned* ctr = nullptr;
-    static int32_t* ovf = nullptr;
-    static uint32_t* ws = nullptr;
-    static int cur_dev = -1;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    const int ovf_cap = 1 << 16, ws_waves = 256, ws_slots = 16384;
-    if (!ctr || cur_dev != dev) {
-        if (dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
-            return BGX_E_HIP;
-        HIP_TRY(hipMemset(ctr, 0, 32));
-        cur_dev = dev;
-    }
-    bgx::MovegenArgs a{};
-    a.n_jobs = n;
-    a.in_mode = bgx::IN_U8;
-    a.in_u8 = d_boards;
-    a.in_player = d_player;
-    a.in_dice = d_dice;
-    a.out_mode = bgx::OUT_U8;
-    a.cap = cap;
-    a.out_u8 = d_out_boards;
-    a.out_count = d_out_count;
-    a.ovf_count = ctr;
-    a.ovf_list = ovf;
-    a.ovf_cap = ovf_cap;
-    a.ws_global = ws;
-    a.ws_waves = ws_waves;
-    a.ws_slots = ws_slots;
-    a.ws_words_per_wave = (size_t)5 * ws_slots;
-    a.err_flags = ctr + 1;
-    HIP_TRY(bgx_launch_movegen(&a, (hipStream_t)stream));
-    return BGX_OK;
+    return guarded("bgx_movegen", [&]() -> int {
+        if (n < 0 || cap < 0) return fail(BGX_E_ARG, "bgx_movegen: n=%d cap=%d", n, cap);
+        if (n == 0) return BGX_OK;
+        if (!d_boards || !d_player || !d_dice || !d_out_count || (cap > 0 && !d_out_boards))
+            return fail(BGX_E_ARG, "bgx_movegen: null pointer");
+        // per-call scratch for the overflow path (kept across calls)
+        static unsigned* ctr = nullptr;
+        static int32_t* ovf = nullptr;
+        static uint32_t* ws = nullptr;
+        static int cur_dev = -1;
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        const int ovf_cap = 1 << 16, ws_waves = 256, ws_slots = 16384;
+        if (!ctr || cur_dev != dev) {
+            if (dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
+                return BGX_E_HIP;
+            HIP_TRY(hipMemset(ctr, 0, 32));
+            cur_dev = dev;
+        }
+        bgx::MovegenArgs a{};
+        a.n_jobs = n;
+        a.in_mode = bgx::IN_U8;
+        a.in_u8 = d_boards;
+        a.in_player = d_player;
+        a.in_dice = d_dice;
+        a.out_mode = bgx::OUT_U8;
+        a.cap = cap;
+        a.out_u8 = d_out_boards;
+        a.out_count = d_out_count;
+        a.ovf_count = ctr;
+        a.ovf_list = ovf;
+        a.ovf_cap = ovf_cap;
+        a.ws_global = ws;
+        a.ws_waves = ws_waves;
+        a.ws_slots = ws_slots;
+        a.ws_words_per_wave = (size_t)5 * ws_slots;
+        a.err_flags = ctr + 1;
+        HIP_TRY(bgx_launch_movegen(&a, (hipStream_t)stream));
+        return BGX_OK;
+    });
 }
 
 int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d_out, int layout,
                void* stream) {
-    if (n < 0 || (layout != 0 && layout != 1)) return fail(BGX_E_ARG, "bgx_encode: n=%d layout=%d", n, layout);
-    if (n == 0) return BGX_OK;
-    if (!d_boards || !d_player || !d_out) return fail(BGX_E_ARG, "bgx_encode: null pointer");
-    HIP_TRY(bgx_launch_encode(d_boards, d_player, n, d_out, layout, (hipStream_t)stream));
-    return BGX_OK;
+    return guarded("bgx_encode", [&]() -> int {
+        if (n < 0 || (layout != 0 && layout != 1)) return fail(BGX_E_ARG, "bgx_encode: n=%d layout=%d", n, layout);
+        if (n == 0) return BGX_OK;
+        if (!d_boards || !d_player || !d_out) return fail(BGX_E_ARG, "bgx_encode: null pointer");
+        HIP_TRY(bgx_launch_encode(d_boards, d_player, n, d_out, layout, (hipStream_t)stream));
+        return BGX_OK;
+    });
 }
 
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream) {
-    if (n < 0) return fail(BGX_E_ARG, "bgx_pack: n=%d", n);
-    HIP_TRY(bgx_launch_pack(d_boards, d_player, n, d_packed, (hipStream_t)stream));
-    return BGX_OK;
+    return guarded("bgx_pack", [&]() -> int {
+        if (n < 0) return fail(BGX_E_ARG, "bgx_pack: n=%d", n);
+        HIP_TRY(bgx_launch_pack(d_boards, d_player, n, d_packed, (hipStream_t)stream));
+        return BGX_OK;
+    });
 }
 
 int bgx_unpack(const uint32_t* d_packed, int n, uint8_t* d_boards, void* stream) {
-    if (n < 0) return fail(BGX_E_ARG, "bgx_unpack: n=%d", n);
-    HIP_TRY(bgx_launch_unpack(d_packed, n, d_boards, (hipStream_t)stream));
-    return BGX_OK;
+    return guarded("bgx_unpack", [&]() -> int {
+        if (n < 0) return fail(BGX_E_ARG, "bgx_unpack: n=%d", n);
+        HIP_TRY(bgx_launch_unpack(d_packed, n, d_boards, (hipStream_t)stream));
+        return BGX_OK;
+    });
 }
 
 int bgx_net_create(const float* h_W1, const float* h_b1, const float* h_w2, const float* h_b2,
                    bgx_net** out) {
-    if (!h_W1 || !h_b1 || !h_w2 || !h_b2 || !out) return fail(BGX_E_ARG, "bgx_net_create: null pointer");
-    bgx_net* n = new bgx_net();
-    if (dalloc(&n->W1, 128 * 198) || dalloc(&n->b1, 128) || dalloc(&n->w2, 128) ||
-        dalloc(&n->wfrag, NFRAG) || dalloc(&n->rowc, 128 * 4)) {
-        bgx_net_destroy(n);
-        return BGX_E_HIP;
-    }
-    int rc = net_upload(n, h_W1, h_b1, h_w2, h_b2);
-    if (rc) {
-        bgx_net_destroy(n);
-        return rc;
-    }
-    *out = n;
-    return BGX_OK;
+    return guarded("bgx_net_create", [&]() -> int {
+        if (!h_W1 || !h_b1 || !h_w2 || !h_b2 || !out) return fail(BGX_E_ARG, "bgx_net_create: null pointer");
+        bgx_net* n = new bgx_net();
+        if (dalloc(&n->W1, 128 * 198) || dalloc(&n->b1, 128) || dalloc(&n->w2, 128) ||
+            dalloc(&n->wfrag, NFRAG) || dalloc(&n->rowc, 128 * 4)) {
+            bgx_net_destroy(n);
+            return BGX_E_HIP;
+        }
+        int rc = net_upload(n, h_W1, h_b1, h_w2, h_b2);
+        if (rc) {
+            bgx_net_destroy(n);
+            return rc;
+        }
+        *out = n;
+        return BGX_OK;
+    });
 }
 
 int bgx_net_destroy(bgx_net* n) {
-    if (!n) return BGX_OK;
-    hipFree(n->W1);
-    hipFree(n->b1);
-    hipFree(n->w2);
-    hipFree(n->wfrag);
-    hipFree(n->rowc);
-    hipFree(n->scratch);
-    delete n;
-    return BGX_OK;
+    return guarded("bgx_net_destroy", [&]() -> int {
+        if (!n) return BGX_OK;
+        hipFree(n->W1);
+        hipFree(n->b1);
+        hipFree(n->w2);
+        hipFree(n->wfrag);
+        hipFree(n->rowc);
+        hipFree(n->scratch);
+        delete n;
+        return BGX_OK;
+    });
 }
 
 int bgx_value(const bgx_net* net, const float* d_x, int n, float* d_out, void* stream) {
-    if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value: bad arguments");
-    if (n == 0) return BGX_OK;
-    HIP_TRY(bgx_launch_value_f32(d_x, n, net->W1, net->b1, net->w2, net->b2, d_out, (hipStream_t)stream));
-    return BGX_OK;
+    return guarded("bgx_value", [&]() -> int {
+        if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value: bad arguments");
+        if (n == 0) return BGX_OK;
+        HIP_TRY(bgx_launch_value_f32(d_x, n, net->W1, net->b1, net->w2, net->b2, d_out, (hipStream_t)stream));
+        return BGX_OK;
+    });
 }
 
 int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t* d_player, int n,
                      float* d_out, void* stream) {
-    bgx_net* net = const_cast<bgx_net*>(cnet);
-    if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value_boards: bad arguments");
-    if (n == 0) return BGX_OK;
-    if (net->scratch_n < n) {
-        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-        hipFree(net->scratch);
-        net->scratch = nullptr;
-        if (dalloc(&net->scratch, (size_t)n * 8)) return BGX_E_HIP;
-        net->scratch_n = n;
-    }
-    HIP_TRY(bgx_launch_pack(d_boards, d_player, n, net->scratch, (hipStream_t)stream));
-    bgx::MlpArgs m{};
-    m.rows = net->scratch;
-    m.n_rows = n;
-    m.out = d_out;
-    m.wfrag = net->wfrag;
-    m.rowc = net->rowc;
-    m.b2 = net->b2;
-    m.feat_scale = net->feat_scale;
-    HIP_TRY(bgx_launch_mlp(&m, (hipStream_t)stream));
-    return BGX_OK;
-}
-
-int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
-                double* d_out, void* stream) {
-    return bgx_two_ply_sampled(net, d_boards, d_opponent, n, 0, 0, d_out, stream);
-}
-
-int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
-                        int sample_k, uint64_t seed, double* d_out, void* stream) {
-    if (!net || n < 0) return fail(BGX_E_ARG, "bgx_two_ply: bad arguments");
-    if (sample_k != 0 && (sample_k < 5 || sample_k > 1024))
-        return fail(BGX_E_ARG, "bgx_two_ply_sampled: sample_k=%d (0 = exact, 5..1024)", sample_k);
-    if (n == 0) return BGX_OK;
-    if (!d_boards || !d_opponent || !d_out) return fail(BGX_E_ARG, "bgx_two_ply: null pointer");
-    hipStream_t s = (hipStream_t)stream;
-    const int jobs = n * 21;
-    const int cap = jobs * 768;   // >= any reply count per (board, roll)
-    uint8_t* mover = nullptr;
-    uint32_t *rows = nullptr, *reply = nullptr, *ws = nullptr;
-    unsigned* ctr = nullptr;
-    int32_t *off = nullptr, *cnt = nullptr, *ovf = nullptr;
-    float *V = nullptr, *jv = nullptr;
-    int rc = BGX_OK;
-    const int ws_waves = 64, ws_slots = 16384, ovf_cap = 1 << 16;
-    if (dalloc(&mover, n) || dalloc(&rows, (size_t)n * 8) || dalloc(&reply, (size_t)cap * 8) ||
-        dalloc(&ctr, 8) || dalloc(&off, jobs) || dalloc(&cnt, jobs) || dalloc(&V, cap) || dalloc(&jv, jobs) ||
-        dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots)) {
-        rc = BGX_E_HIP;
-    }
-    std::vector<uint8_t> hm;
-    if (!rc) {
-        // the candidate board's indicator = the player who just moved = 1 - opponent
-        std::vector<uint8_t> ho(n);
-        if (hipMemcpy(ho.data(), d_opponent, n, hipMemcpyDeviceToHost) != hipSuccess) rc = BGX_E_HIP;
-        hm.resize(n);
-        for (int i = 0; i < n; ++i) hm[i] = (uint8_t)(1 - (ho[i] & 1));
-    }
-    if (!rc && hipMemcpy(mover, hm.data(), n, hipMemcpyHostToDevice) != hipSuccess) rc = BGX_E_HIP;
-    if (!rc && hipMemsetAsync(ctr, 0, 32, s) != hipSuccess) rc = BGX_E_HIP;
-    if (!rc && bgx_launch_pack(d_boards, mover, n, rows, s) != hipSuccess) rc = BGX_E_HIP;
-    if (!rc) {
-        bgx::MovegenArgs b{};
-        b.n_jobs = jobs;
-        b.in_mode = bgx::IN_TWOPLY;
-        b.in_packed = rows;
-        b.in_rows = nullptr;
-        b.in_row_base = 0;
-        b.out_mode = bgx::OUT_PACKED_FLAT;
-        b.out_packed = reply;
-        b.flat_count = ctr;
-        b.flat_cap = cap;
-        b.flat_chunk = 256;
-        b.job_off = off;
-        b.job_cnt = cnt;
-        b.ovf_count = ctr + 2;
-        b.ovf_list = ovf;
-        b.ovf_cap = ovf_cap;
-        b.ws_global = ws;
-        b.ws_waves = ws_waves;
-        b.ws_slots = ws_slots;
-        b.ws_words_per_wave = (size_t)5 * ws_slots;
-        b.err_flags = ctr + 3;
-        if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
-    }
-    if (!rc) {
+    return guarded("bgx_value_boards", [&]() -> int {
+        bgx_net* net = const_cast<bgx_net*>(cnet);
+        if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value_boards: bad arguments");
+        if (n == 0) return BGX_OK;
+        if (net->scratch_n < n) {
+            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+            hipFree(net->scratch);
+            net->scratch = nullptr;
+            if (dalloc(&net->scratch, (size_t)n * 8)) return BGX_E_HIP;
+            net->scratch_n = n;
+        }
+        HIP_TRY(bgx_launch_pack(d_boards, d_player, n, net->scratch, (hipStream_t)stream));
         bgx::MlpArgs m{};
-        m.rows = reply;
-        m.n_rows = 0;
-        m.n_rows_dev = ctr;
-        m.n_max = cap;
-        m.nt = 2;
-        m.out = V;
+        m.rows = net->scratch;
+        m.n_rows = n;
+        m.out = d_out;
         m.wfrag = net->wfrag;
         m.rowc = net->rowc;
         m.b2 = net->b2;
         m.feat_scale = net->feat_scale;
-        if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
-    }
-    if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, sample_k, seed, nullptr, s) != hipSuccess)
-        rc = BGX_E_HIP;
-    if (!rc && bgx_launch_two_ply_reduce(jv, n, d_out, s) != hipSuccess) rc = BGX_E_HIP;
-    unsigned flags = 0;
-    if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
-        rc = BGX_E_HIP;
-    void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws};
-    for (void* p : ps) hipFree(p);
-    if (rc) return fail(rc, "bgx_two_ply: HIP failure");
-    if (flags) return fail(BGX_E_CAPACITY, "bgx_two_ply: overflow flags 0x%x", flags);
-    return BGX_OK;
+        HIP_TRY(bgx_launch_mlp(&m, (hipStream_t)stream));
+        return BGX_OK;
+    });
+}
+
+int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
+                double* d_out, void* stream) {
+    return guarded("bgx_two_ply", [&]() -> int {
+        return bgx_two_ply_sampled(net, d_boards, d_opponent, n, 0, 0, d_out, stream);
+    });
+}
+
+int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
+                        int sample_k, uint64_t seed, double* d_out, void* stream) {
+    return guarded("bgx_two_ply_sampled", [&]() -> int {
+        if (!net || n < 0) return fail(BGX_E_ARG, "bgx_two_ply: bad arguments");
+        if (sample_k != 0 && (sample_k < 5 || sample_k > 1024))
+            return fail(BGX_E_ARG, "bgx_two_ply_sampled: sample_k=%d (0 = exact, 5..1024)", sample_k);
+        if (n == 0) return BGX_OK;
+        if (!d_boards || !d_opponent || !d_out) return fail(BGX_E_ARG, "bgx_two_ply: null pointer");
+        hipStream_t s = (hipStream_t)stream;
+        const int jobs = n * 21;
+        const int cap = jobs * 768;   // >= any reply count per (board, roll)
+        uint8_t* mover = nullptr;
+        uint32_t *rows = nullptr, *reply = nullptr, *ws = nullptr;
+        unsigned* ctr = nullptr;
+        int32_t *off = nullptr, *cnt = nullptr, *ovf = nullptr;
+        float *V = nullptr, *jv = nullptr;
+        int rc = BGX_OK;
+        const int ws_waves = 64, ws_slots = 16384, ovf_cap = 1 << 16;
+        if (dalloc(&mover, n) || dalloc(&rows, (size_t)n * 8) || dalloc(&reply, (size_t)cap * 8) ||
+            dalloc(&ctr, 8) || dalloc(&off, jobs) || dalloc(&cnt, jobs) || dalloc(&V, cap) || dalloc(&jv, jobs) ||
+            dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots)) {
+            rc = BGX_E_HIP;
+        }
+        std::vector<uint8_t> hm;
+        if (!rc) {
+            // the candidate board's indicator = the player who just moved = 1 - opponent
+            std::vector<uint8_t> ho(n);
+            if (hipMemcpy(ho.data(), d_opponent, n, hipMemcpyDeviceToHost) != hipSuccess) rc = BGX_E_HIP;
+            hm.resize(n);
+            for (int i = 0; i < n; ++i) hm[i] = (uint8_t)(1 - (ho[i] & 1));
+        }
+        if (!rc && hipMemcpy(mover, hm.data(), n, hipMemcpyHostToDevice) != hipSuccess) rc = BGX_E_HIP;
+        if (!rc && hipMemsetAsync(ctr, 0, 32, s) != hipSuccess) rc = BGX_E_HIP;
+        if (!rc && bgx_launch_pack(d_boards, mover, n, rows, s) != hipSuccess) rc = BGX_E_HIP;
+        if (!rc) {
+            bgx::MovegenArgs b{};
+            b.n_jobs = jobs;
+            b.in_mode = bgx::IN_TWOPLY;
+            b.in_packed = rows;
+            b.in_rows = nullptr;
+            b.in_row_base = 0;
+            b.out_mode = bgx::OUT_PACKED_FLAT;
+            b.out_packed = reply;
+            b.flat_count = ctr;
+            b.flat_cap = cap;
+            b.flat_chunk = 256;
+            b.job_off = off;
+            b.job_cnt = cnt;
+            b.ovf_count = ctr + 2;
+            b.ovf_list = ovf;
+            b.ovf_cap = ovf_cap;
+            b.ws_global = ws;
+            b.ws_waves = ws_waves;
+            b.ws_slots = ws_slots;
+            b.ws_words_per_wave = (size_t)5 * ws_slots;
+            b.err_flags = ctr + 3;
+            if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
+        }
+        if (!rc) {
+            bgx::MlpArgs m{};
+            m.rows = reply;
+            m.n_rows = 0;
+            m.n_rows_dev = ctr;
+            m.n_max = cap;
+            m.nt = 2;
+            m.out = V;
+            m.wfrag = net->wfrag;
+            m.rowc = net->rowc;
+            m.b2 = net->b2;
+            m.feat_scale = net->feat_scale;
+            if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
+        }
+        if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, sample_k, seed, nullptr, s) != hipSuccess)
+            rc = BGX_E_HIP;
+        if (!rc && bgx_launch_two_ply_reduce(jv, n, d_out, s) != hipSuccess) rc = BGX_E_HIP;
+        unsigned flags = 0;
+        if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
+            rc = BGX_E_HIP;
+        void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws};
+        for (void* p : ps) hipFree(p);
+        if (rc) return fail(rc, "bgx_two_ply: HIP failure");
+        if (flags) return fail(BGX_E_CAPACITY, "bgx_two_ply: overflow flags 0x%x", flags);
+        return BGX_OK;
+    });
 }
 
 void bgx_config_default(bgx_config* c) {
@@ -406,7 +461,7 @@ void bgx_config_default(bgx_config* c) {
     c->beta = 0.9f;
     c->max_steps = 300;
     c->max_legal = 500;
-    c->ring = 640;
+    c->ring = 1024;
     c->ep_cap = 0;   // 0 = derived from lanes
     c->cand_per_lane = 256;
     c->reply_per_lane = 0;   // 0 = derived from k_top
@@ -414,183 +469,234 @@ void bgx_config_default(bgx_config* c) {
 }
 
 int bgx_engine_destroy(bgx_engine* e) {
-    if (!e) return BGX_OK;
-    hipSetDevice(e->device);
-    hipDeviceSynchronize();
-    if (e->fprof) {   // development report (BGX_FUSED_PROF): per workgroup-step averages, wall clock 100 MHz
-        std::vector<unsigned long long> p((size_t)1024 * 16);
-        if (hipMemcpy(p.data(), e->fprof, p.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-            double s[16] = {0};
-            for (int b = 0; b < 1024; ++b)
-                for (int k = 0; k < 14; ++k) s[k] += (double)p[(size_t)b * 16 + k];
-            const double n = s[5] > 0 ? s[5] : 1;
-            fprintf(stderr, "[bgx fused prof] us per workgroup step: step+tier1 %.2f tier2 %.2f wload %.2f mlp %.2f "
-                    "pick %.2f | mean wave tier-1 job %.2f (%0.f workgroup steps)\n",
-                    s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n / 100, s[4] / n / 100,
-                    s[6] / n / 16 / 100, n);
-            fprintf(stderr, "[bgx fused prof] mean per wave-step: mlp %.2f | -- %.2f pick %.2f "
-                    "advance %.2f us\n", s[7] / n / 16 / 100, s[8] / n / 16 / 100, s[9] / n / 16 / 100,
-                    s[10] / n / 16 / 100);
-            fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
-                    s[11] / (s[12] > 0 ? s[12] : 1) / 100);
+    return guarded("bgx_engine_destroy", [&]() -> int {
+        if (!e) return BGX_OK;
+        hipSetDevice(e->device);
+        hipDeviceSynchronize();
+        if (e->fprof) {   // development report (BGX_FUSED_PROF): per workgroup-step averages, wall clock 100 MHz
+            std::vector<unsigned long long> p((size_t)1024 * 16);
+            if (hipMemcpy(p.data(), e->fprof, p.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                double s[16] = {0};
+                for (int b = 0; b < 1024; ++b)
+                    for (int k = 0; k < 14; ++k) s[k] += (double)p[(size_t)b * 16 + k];
+                const double n = s[5] > 0 ? s[5] : 1;
+                fprintf(stderr, "[bgx fused prof] us per workgroup step: step+tier1 %.2f tier2 %.2f wload %.2f mlp %.2f "
+                        "pick %.2f | mean wave tier-1 job %.2f (%0.f workgroup steps)\n",
+                        s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n / 100, s[4] / n / 100,
+                        s[6] / n / 16 / 100, n);
+                fprintf(stderr, "[bgx fused prof] mean per wave-step: mlp %.2f | -- %.2f pick %.2f "
+                        "advance %.2f us\n", s[7] / n / 16 / 100, s[8] / n / 16 / 100, s[9] / n / 16 / 100,
+                        s[10] / n / 16 / 100);
+                fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
+                        s[11] / (s[12] > 0 ? s[12] : 1) / 100);
+            }
+            hipFree(e->fprof);
         }
-        hipFree(e->fprof);
-    }
-    void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
-                  e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
-                  e->d_offs, e->d_info, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
-                  e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list};
-    for (void* p : ps) hipFree(p);
-    for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
-    if (e->gexec) hipGraphExecDestroy(e->gexec);
-    if (e->hev) hipEventDestroy(e->hev);
-    if (e->h_info) hipHostFree(e->h_info);
-    if (e->cap) hipStreamDestroy(e->cap);
-    bgx_net_destroy(e->net);
-    delete e;
-    return BGX_OK;
+        void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
+                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
+                      e->d_offs, e->d_info, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
+                      e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->dice_tab};
+        for (void* p : ps) hipFree(p);
+        for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+        if (e->gexec) hipGraphExecDestroy(e->gexec);
+        if (e->hev) hipEventDestroy(e->hev);
+        if (e->h_info) hipHostFree(e->h_info);
+        if (e->cap) hipStreamDestroy(e->cap);
+        bgx_net_destroy(e->net);
+        delete e;
+        return BGX_OK;
+    });
 }
 
 int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
-    if (!cfg || !out) return fail(BGX_E_ARG, "bgx_engine_create: null pointer");
-    if (cfg->lanes <= 0 || cfg->lanes > (1 << 24)) return fail(BGX_E_ARG, "lanes=%d", cfg->lanes);
-    if (cfg->ply != 1 && cfg->ply != 2) return fail(BGX_E_ARG, "ply=%d (1 or 2)", cfg->ply);
-    if (cfg->ply == 2 && cfg->k_top != 4 && cfg->k_top != 0)
-        return fail(BGX_E_ARG, "k_top=%d (4 = reference, 0 = all)", cfg->k_top);
-    if (cfg->reply_sample != 0 && (cfg->reply_sample < 5 || cfg->reply_sample > 1024))
-        return fail(BGX_E_ARG, "reply_sample=%d (0 = exact, 5..1024; the reference samples 50)", cfg->reply_sample);
-    if (cfg->max_steps <= 0 || cfg->max_legal <= 0) return fail(BGX_E_ARG, "max_steps/max_legal");
-    if (cfg->ring < cfg->max_steps + 1) return fail(BGX_E_ARG, "ring=%d < max_steps+1", cfg->ring);
-    HIP_TRY(hipSetDevice(device));
-    bgx_engine* e = new bgx_engine();
-    e->device = device;
-    if (const char* g = getenv("BGX_GRAPH")) e->use_graph = atoi(g) != 0;
-    e->cfg = *cfg;
-    const int L = cfg->lanes;
-    e->cand_cap = L * (cfg->cand_per_lane > 0 ? cfg->cand_per_lane : 256);
-    const int ep_cap = cfg->ep_cap > 0 ? cfg->ep_cap : 4 * L + 1024;
-    int rc = BGX_OK;
-    bgx::EngineDev& d = e->d;
-#define ALLOC(p, n) \
-    if (!rc) rc = dalloc(&(p), (size_t)(n))
-    ALLOC(e->rows, (size_t)(L + e->cand_cap) * 8);
-    ALLOC(e->V, (size_t)(L + e->cand_cap));
-    ALLOC(e->cand_off, L);
-    ALLOC(e->cand_cnt, L);
-    ALLOC(e->ctr, 16);
-    ALLOC(e->stats, 8);
-    ALLOC(d.player, L);
-    ALLOC(d.dice, 2 * L);
-    ALLOC(d.step, L);
-    ALLOC(d.flags, L);
-    ALLOC(d.epi, L);
-    ALLOC(d.rng, L);
-    ALLOC(d.rec_count, L);
-    ALLOC(d.ep_first, L);
-    ALLOC(d.harv, L);
-    ALLOC(d.ring, (size_t)L * cfg->ring * bgx::REC_WORDS);
-    ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
-    ALLOC(e->out_records, (size_t)L * cfg->ring * bgx::REC_WORDS);
-    ALLOC(e->d_offs, (size_t)ep_cap + 1);
-    ALLOC(e->d_info, 4);
-    if (!rc && hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
-        rc = fail(BGX_E_HIP, "hipHostMalloc failed");
-    e->ovf_cap = 1 << 16;
-    e->ws_waves = 256;   // one global-memory fallback slice per tier-2 block
-    e->ws_slots = 16384;
-    ALLOC(e->ovf_list, e->ovf_cap);
-    ALLOC(e->ws, (size_t)e->ws_waves * 5 * e->ws_slots);
-    e->fused = cfg->fused != 0 && cfg->ply == 1;
-    if (e->fused) {
-        e->fcap = cfg->max_legal;
-        if (e->fcap > 2048) {
-            bgx_engine_destroy(e);
-            return fail(BGX_E_ARG, "fused engine: max_legal=%d > 2048", cfg->max_legal);
+    return guarded("bgx_engine_create", [&]() -> int {
+        if (!cfg || !out) return fail(BGX_E_ARG, "bgx_engine_create: null pointer");
+        if (cfg->lanes <= 0 || cfg->lanes > (1 << 24)) return fail(BGX_E_ARG, "lanes=%d", cfg->lanes);
+        if (cfg->ply != 1 && cfg->ply != 2) return fail(BGX_E_ARG, "ply=%d (1 or 2)", cfg->ply);
+        if (cfg->ply == 2 && cfg->k_top != 4 && cfg->k_top != 0)
+            return fail(BGX_E_ARG, "k_top=%d (4 = reference, 0 = all)", cfg->k_top);
+        if (cfg->reply_sample != 0 && (cfg->reply_sample < 5 || cfg->reply_sample > 1024))
+            return fail(BGX_E_ARG, "reply_sample=%d (0 = exact, 5..1024; the reference samples 50)", cfg->reply_sample);
+        if (cfg->max_steps <= 0 || cfg->max_legal <= 0) return fail(BGX_E_ARG, "max_steps/max_legal");
+        if (cfg->ring < cfg->max_steps + 1 || cfg->ring > (1 << 16))
+            return fail(BGX_E_ARG, "ring=%d (max_steps+1 .. 65536)", cfg->ring);
+        // the select kernel keeps a lane's scores in a 512-entry LDS row; the fused
+        // 1-ply kernel keeps its candidates in per-lane slots of max_legal
+        const bool fused_cfg = cfg->fused != 0 && cfg->ply == 1;
+        if (cfg->max_legal > (fused_cfg ? 2048 : 512))
+            return fail(BGX_E_ARG, "max_legal=%d > %d (%s engine)", cfg->max_legal, fused_cfg ? 2048 : 512,
+                        fused_cfg ? "fused" : "phased");
+        if (cfg->max_steps > 511) return fail(BGX_E_ARG, "max_steps=%d > 511 (record step field)", cfg->max_steps);
+        HIP_TRY(hipSetDevice(device));
+        bgx_engine* e = new bgx_engine();
+        e->device = device;
+        if (const char* g = getenv("BGX_GRAPH")) e->use_graph = atoi(g) != 0;
+        if (const char* v = getenv("BGX_MG_TEST_TIER")) e->force_tier = atoi(v);
+        e->prof_enabled = getenv("BGX_FUSED_PROF") != nullptr;
+        e->cfg = *cfg;
+        // ring slots: a power of two (slot = record counter & (R - 1) stays exact
+        // when the 32-bit counter wraps)
+        int ring = 1;
+        while (ring < cfg->ring) ring <<= 1;
+        e->cfg.ring = ring;
+        const int L = cfg->lanes;
+        e->cand_cap = L * (cfg->cand_per_lane > 0 ? cfg->cand_per_lane : 256);
+        // finished episodes between two harvests: at most (steps per harvest) /
+        // (shortest game) + 1 per lane. A game takes >= 7 turns of the winner
+        // (167 pips, at most 24 per turn) and >= 6 of the loser: >= 13 env steps.
+        constexpr int kMinGameSteps = 13;
+        const long long ep_need = (long long)L * ((ring - cfg->max_steps) / kMinGameSteps + 1) + 1024;
+        const int ep_cap = cfg->ep_cap > 0 ? cfg->ep_cap : (int)(ep_need < (1 << 30) ? ep_need : (1 << 30));
+        int rc = BGX_OK;
+        bgx::EngineDev& d = e->d;
+    #define ALLOC(p, n) \
+        if (!rc) rc = dalloc(&(p), (size_t)(n))
+        ALLOC(e->rows, (size_t)(L + e->cand_cap) * 8);
+        ALLOC(e->V, (size_t)(L + e->cand_cap));
+        ALLOC(e->cand_off, L);
+        ALLOC(e->cand_cnt, L);
+        ALLOC(e->ctr, 16);
+        ALLOC(e->stats, 8);
+        ALLOC(d.player, L);
+        ALLOC(d.dice, 2 * L);
+        ALLOC(d.step, L);
+        ALLOC(d.flags, L);
+        ALLOC(d.epi, L);
+        ALLOC(d.rng, L);
+        ALLOC(d.rec_count, L);
+        ALLOC(d.ep_first, L);
+        ALLOC(d.harv, L);
+        ALLOC(d.ring, (size_t)L * ring * bgx::REC_WORDS);
+        ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
+        ALLOC(e->out_records, (size_t)L * ring * bgx::REC_WORDS);
+        ALLOC(e->d_offs, (size_t)ep_cap + 1);
+        ALLOC(e->d_info, 4);
+        if (!rc && hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+            rc = fail(BGX_E_HIP, "hipHostMalloc failed");
+        e->ovf_cap = 1 << 16;
+        e->ws_waves = 256;   // one global-memory fallback slice per tier-2 block
+        e->ws_slots = 16384;
+        ALLOC(e->ovf_list, e->ovf_cap);
+        ALLOC(e->ws, (size_t)e->ws_waves * 5 * e->ws_slots);
+        e->fused = fused_cfg;
+        if (e->fused) {
+            e->fcap = cfg->max_legal;
+            ALLOC(e->fcand, (size_t)L * e->fcap * 8);
+            ALLOC(e->fvbuf, (size_t)L * (e->fcap + 1));
         }
-        ALLOC(e->fcand, (size_t)L * e->fcap * 8);
-        ALLOC(e->fvbuf, (size_t)L * (e->fcap + 1));
-    }
-    if (cfg->ply == 2) {
-        e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
-        const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
-        int n_cu = 256;
-        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) n_cu = 256;
-        // + the slack of one partly used 512-row reservation per resident movegen wave (<= 32 / CU)
-        e->reply_cap = L * per_lane + n_cu * 32 * 512;
-        ALLOC(e->sel, 4 * L);
-        ALLOC(e->sel_rows, (size_t)4 * L * 8);
-        ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
-        ALLOC(e->reply_V, e->reply_cap);
-        ALLOC(e->job_off, e->jobs_cap);
-        ALLOC(e->job_cnt, e->jobs_cap);
-        ALLOC(e->job_val, e->jobs_cap);
-    }
-#undef ALLOC
-    if (rc) {
-        bgx_engine_destroy(e);
-        return rc;
-    }
-    if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess) {
-        bgx_engine_destroy(e);
-        return fail(BGX_E_HIP, "hipMemset failed");
-    }
-    d.L = L;
-    d.lane_base = cfg->lane_base;
-    d.seed = cfg->seed;
-    d.temperature = 1.5f;
-    d.max_steps = cfg->max_steps;
-    d.max_legal = cfg->max_legal;
-    d.ply = cfg->ply;
-    d.k_top = cfg->k_top;
-    d.alpha = cfg->alpha;
-    d.greedy = cfg->greedy != 0;
-    d.beta = cfg->beta;
-    d.rows = e->rows;
-    d.cand_cap = e->cand_cap;
-    d.R = cfg->ring;
-    d.ep_count = e->ctr + C_EP;
-    d.ep_cap = ep_cap;
-    d.cand_off = e->cand_off;
-    d.cand_cnt = e->cand_cnt;
-    d.V = e->V;
-    d.sel = e->sel;
-    d.sel_rows = e->sel_rows;
-    d.job_val = e->job_val;
-    d.flat_count = e->ctr + C_FLAT;
-    d.reply_count = e->ctr + C_REPLY;
-    d.ovf_count = e->ctr + C_OVF;
-    d.ovf_count2 = e->ctr + C_OVF2;
-    d.n_jobs2 = cfg->k_top == 4 ? L * 4 * 21 : 0;
-    d.stats = e->stats;
-    d.err_flags = e->ctr + C_ERR;
-    if (bgx_launch_engine_reset(&d, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        bgx_engine_destroy(e);
-        return fail(BGX_E_HIP, "engine reset failed");
-    }
-    *out = e;
-    return BGX_OK;
+        if (cfg->ply == 2) {
+            e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
+            const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
+            int n_cu = 256;
+            if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) n_cu = 256;
+            // + the slack of one partly used 512-row reservation per resident movegen wave (<= 32 / CU)
+            e->reply_cap = L * per_lane + n_cu * 32 * 512;
+            ALLOC(e->sel, 4 * L);
+            ALLOC(e->sel_rows, (size_t)4 * L * 8);
+            ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
+            ALLOC(e->reply_V, e->reply_cap);
+            ALLOC(e->job_off, e->jobs_cap);
+            ALLOC(e->job_cnt, e->jobs_cap);
+            ALLOC(e->job_val, e->jobs_cap);
+        }
+    #undef ALLOC
+        if (rc) {
+            bgx_engine_destroy(e);
+            return rc;
+        }
+        if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess) {
+            bgx_engine_destroy(e);
+            return fail(BGX_E_HIP, "hipMemset failed");
+        }
+        d.L = L;
+        d.lane_base = cfg->lane_base;
+        d.seed = cfg->seed;
+        d.temperature = 1.5f;
+        d.max_steps = cfg->max_steps;
+        d.max_legal = cfg->max_legal;
+        d.ply = cfg->ply;
+        d.k_top = cfg->k_top;
+        d.alpha = cfg->alpha;
+        d.greedy = cfg->greedy != 0;
+        d.beta = cfg->beta;
+        d.rows = e->rows;
+        d.cand_cap = e->cand_cap;
+        d.R = ring;
+        d.dice_tab = nullptr;
+        d.dice_len = 0;
+        d.ep_count = e->ctr + C_EP;
+        d.ep_cap = ep_cap;
+        d.cand_off = e->cand_off;
+        d.cand_cnt = e->cand_cnt;
+        d.V = e->V;
+        d.sel = e->sel;
+        d.sel_rows = e->sel_rows;
+        d.job_val = e->job_val;
+        d.flat_count = e->ctr + C_FLAT;
+        d.reply_count = e->ctr + C_REPLY;
+        d.ovf_count = e->ctr + C_OVF;
+        d.ovf_count2 = e->ctr + C_OVF2;
+        d.n_jobs2 = cfg->k_top == 4 ? L * 4 * 21 : 0;
+        d.stats = e->stats;
+        d.err_flags = e->ctr + C_ERR;
+        if (bgx_launch_engine_reset(&d, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            bgx_engine_destroy(e);
+            return fail(BGX_E_HIP, "engine reset failed");
+        }
+        *out = e;
+        return BGX_OK;
+    });
+}
+
+int bgx_engine_set_dice(bgx_engine* e, const uint8_t* h_dice, int per_lane) {
+    return guarded("bgx_engine_set_dice", [&]() -> int {
+        if (!e || !h_dice || per_lane < 2) return fail(BGX_E_ARG, "bgx_engine_set_dice: bad arguments");
+        if (!e->cfg.greedy) return fail(BGX_E_STATE, "bgx_engine_set_dice: scripted dice need greedy play");
+        const size_t n = (size_t)e->cfg.lanes * (size_t)per_lane;
+        for (size_t k = 0; k < n; ++k)
+            if (h_dice[k] < 1 || h_dice[k] > 6) return fail(BGX_E_ARG, "bgx_engine_set_dice: die %d at %zu", h_dice[k], k);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+        hipFree(e->dice_tab);
+        e->dice_tab = nullptr;
+        if (dalloc(&e->dice_tab, n)) return BGX_E_HIP;
+        HIP_TRY(hipMemcpy(e->dice_tab, h_dice, n, hipMemcpyHostToDevice));
+        e->d.dice_tab = e->dice_tab;
+        e->d.dice_len = per_lane;
+        if (e->gexec) {
+            HIP_TRY(hipGraphExecDestroy(e->gexec));
+            e->gexec = nullptr;
+        }
+        // every lane restarts from BackgammonEnv.reset with its scripted dice
+        HIP_TRY(hipMemset(e->ctr, 0, 64));
+        HIP_TRY(bgx_launch_engine_reset(&e->d, nullptr));
+        HIP_TRY(hipDeviceSynchronize());
+        return check_flags(e);
+    });
 }
 
 int bgx_set_weights(bgx_engine* e, const float* h_W1, const float* h_b1, const float* h_w2,
                     const float* h_b2, float temperature, uint64_t version) {
-    (void)version;
-    if (!e) return fail(BGX_E_ARG, "bgx_set_weights: null engine");
-    if (!(temperature > 0.0f)) return fail(BGX_E_ARG, "temperature=%g", (double)temperature);
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
-    if (!e->net) {
-        int rc = bgx_net_create(h_W1, h_b1, h_w2, h_b2, &e->net);
-        if (rc) return rc;
-    } else {
-        int rc = net_upload(e->net, h_W1, h_b1, h_w2, h_b2);
-        if (rc) return rc;
-    }
-    if (e->gexec && e->d.temperature != temperature) {
-        HIP_TRY(hipGraphExecDestroy(e->gexec));
-        e->gexec = nullptr;
-    }
-    e->d.temperature = temperature;
-    return BGX_OK;
+    return guarded("bgx_set_weights", [&]() -> int {
+        (void)version;
+        if (!e) return fail(BGX_E_ARG, "bgx_set_weights: null engine");
+        if (!(temperature > 0.0f)) return fail(BGX_E_ARG, "temperature=%g", (double)temperature);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+        if (!e->net) {
+            int rc = bgx_net_create(h_W1, h_b1, h_w2, h_b2, &e->net);
+            if (rc) return rc;
+        } else {
+            int rc = net_upload(e->net, h_W1, h_b1, h_w2, h_b2);
+            if (rc) return rc;
+        }
+        if (e->gexec && e->d.temperature != temperature) {
+            HIP_TRY(hipGraphExecDestroy(e->gexec));
+            e->gexec = nullptr;
+        }
+        e->d.temperature = temperature;
+        return BGX_OK;
+    });
 }
 
 static void mg_common(bgx_engine* e, bgx::MovegenArgs& a) {
@@ -728,9 +834,8 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.ws_blocks = e->ws_waves;
     f.ws_slots = e->ws_slots;
     f.ws_words_per_block = (size_t)5 * e->ws_slots;
-    if (const char* v = getenv("BGX_MG_TEST_TIER")) f.force_tier = atoi(v);
-    if (const char* v = getenv("BGX_FUSED_EXP")) f.exp = atoi(v);
-    if (getenv("BGX_FUSED_PROF")) {
+    f.force_tier = e->force_tier;
+    if (e->prof_enabled) {
         if (!e->fprof) {
             if (dalloc(&e->fprof, (size_t)1024 * 16)) return BGX_E_HIP;
             HIP_TRY(hipMemset(e->fprof, 0, (size_t)1024 * 16 * 8));
@@ -744,146 +849,147 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
 }
 
 int bgx_step(bgx_engine* e, int n_steps, void* stream) {
-    if (!e || n_steps < 0) return fail(BGX_E_ARG, "bgx_step: bad arguments");
-    if (!e->net) return fail(BGX_E_STATE, "bgx_step: bgx_set_weights first");
-    if (n_steps > e->cfg.ring - e->cfg.max_steps)
-        return fail(BGX_E_ARG, "bgx_step: n_steps=%d > ring - max_steps = %d (harvest more often)", n_steps,
-                    e->cfg.ring - e->cfg.max_steps);
-    HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = (hipStream_t)stream;
-    e->last = s;
-    if (n_steps == 0) return BGX_OK;
-    // timed runs launch directly (events between the kernels); otherwise the
-    // n_steps sequence is one graph launch (kernel arguments are fixed for the
-    // engine's lifetime; bgx_set_weights drops the graph: temperature is an argument)
-    if (e->fused) return enqueue_fused(e, n_steps, s);
-    if (e->timing || !e->use_graph) return enqueue_steps(e, n_steps, s);
-    if (!e->gexec || e->g_steps != n_steps) {
-        if (e->gexec) {
-            HIP_TRY(hipGraphExecDestroy(e->gexec));
-            e->gexec = nullptr;
+    return guarded("bgx_step", [&]() -> int {
+        if (!e || n_steps < 0) return fail(BGX_E_ARG, "bgx_step: bad arguments");
+        if (!e->net) return fail(BGX_E_STATE, "bgx_step: bgx_set_weights first");
+        if (n_steps > e->cfg.ring - e->cfg.max_steps)
+            return fail(BGX_E_ARG, "bgx_step: n_steps=%d > ring - max_steps = %d (harvest more often)", n_steps,
+                        e->cfg.ring - e->cfg.max_steps);
+        HIP_TRY(hipSetDevice(e->device));
+        hipStream_t s = (hipStream_t)stream;
+        e->last = s;
+        if (n_steps == 0) return BGX_OK;
+        // timed runs launch directly (events between the kernels); otherwise the
+        // n_steps sequence is one graph launch (kernel arguments are fixed for the
+        // engine's lifetime; bgx_set_weights drops the graph: temperature is an argument)
+        if (e->fused) return enqueue_fused(e, n_steps, s);
+        if (e->timing || !e->use_graph) return enqueue_steps(e, n_steps, s);
+        if (!e->gexec || e->g_steps != n_steps) {
+            if (e->gexec) {
+                HIP_TRY(hipGraphExecDestroy(e->gexec));
+                e->gexec = nullptr;
+            }
+            if (!e->cap) HIP_TRY(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+            HIP_TRY(hipStreamBeginCapture(e->cap, hipStreamCaptureModeRelaxed));
+            const int rc = enqueue_steps(e, n_steps, e->cap);
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(e->cap, &g);
+            if (rc) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc;
+            }
+            HIP_TRY(ec);
+            const hipError_t ei = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            HIP_TRY(ei);
+            e->g_steps = n_steps;
         }
-        if (!e->cap) HIP_TRY(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
-        HIP_TRY(hipStreamBeginCapture(e->cap, hipStreamCaptureModeRelaxed));
-        const int rc = enqueue_steps(e, n_steps, e->cap);
-        hipGraph_t g = nullptr;
-        const hipError_t ec = hipStreamEndCapture(e->cap, &g);
-        if (rc) {
-            if (g) (void)hipGraphDestroy(g);
-            return rc;
-        }
-        HIP_TRY(ec);
-        const hipError_t ei = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        HIP_TRY(ei);
-        e->g_steps = n_steps;
-    }
-    HIP_TRY(hipGraphLaunch(e->gexec, s));
-    return BGX_OK;
-}
-
-static int check_flags(bgx_engine* e) {
-    unsigned f = 0;
-    HIP_TRY(hipMemcpy(&f, e->ctr + C_ERR, 4, hipMemcpyDeviceToHost));
-    if (f) {
-        HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
-        return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
-                    "workspace, 8 experience ring, 16 episode list)", f);
-    }
-    return BGX_OK;
+        HIP_TRY(hipGraphLaunch(e->gexec, s));
+        return BGX_OK;
+    });
 }
 
 int bgx_sync(bgx_engine* e) {
-    if (!e) return fail(BGX_E_ARG, "bgx_sync: null engine");
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->last));
-    return check_flags(e);
+    return guarded("bgx_sync", [&]() -> int {
+        if (!e) return fail(BGX_E_ARG, "bgx_sync: null engine");
+        HIP_TRY(hipSetDevice(e->device));
+        HIP_TRY(hipStreamSynchronize(e->last));
+        return check_flags(e);
+    });
 }
 
 int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
-    if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest: null pointer");
-    HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = (hipStream_t)stream;
-    // order after the engine's last step (another stream): an event, no host wait
-    if (e->last != s) {
-        if (!e->hev) HIP_TRY(hipEventCreateWithFlags(&e->hev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(e->hev, e->last));
-        HIP_TRY(hipStreamWaitEvent(s, e->hev, 0));
-    }
-    // offsets and totals on the device (harvest_scan_kernel), gather, then ONE
-    // small copy of {episodes, records, error flags} to the host
-    HIP_TRY(bgx_launch_harvest(&e->d, e->d_offs, e->d_info, e->out_records, s));
-    HIP_TRY(hipMemcpyAsync(e->h_info, e->d_info, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const uint32_t flags = e->h_info[2];
-    if (flags) {
-        HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
-        return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
-                    "workspace, 8 experience ring, 16 episode list)", flags);
-    }
-    out->n_episodes = (int)e->h_info[0];
-    out->n_records = (int)e->h_info[1];
-    out->d_headers = e->d.ep_list;
-    out->d_records = e->out_records;
-    return BGX_OK;
+    return guarded("bgx_harvest", [&]() -> int {
+        if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest: null pointer");
+        HIP_TRY(hipSetDevice(e->device));
+        hipStream_t s = (hipStream_t)stream;
+        // order after the engine's last step (another stream): an event, no host wait
+        if (e->last != s) {
+            if (!e->hev) HIP_TRY(hipEventCreateWithFlags(&e->hev, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(e->hev, e->last));
+            HIP_TRY(hipStreamWaitEvent(s, e->hev, 0));
+        }
+        // offsets and totals on the device (harvest_scan_kernel), gather, then ONE
+        // small copy of {episodes, records, error flags} to the host
+        HIP_TRY(bgx_launch_harvest(&e->d, e->d_offs, e->d_info, e->out_records, s));
+        HIP_TRY(hipMemcpyAsync(e->h_info, e->d_info, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint32_t flags = e->h_info[2];
+        if (flags) {
+            HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
+            return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
+                        "workspace, 8 experience ring, 16 episode list, 32 scripted dice)", flags);
+        }
+        out->n_episodes = (int)e->h_info[0];
+        out->n_records = (int)e->h_info[1];
+        out->d_headers = e->d.ep_list;
+        out->d_records = e->out_records;
+        return BGX_OK;
+    });
 }
 
 int bgx_get_stats(bgx_engine* e, bgx_stats* out) {
-    if (!e || !out) return fail(BGX_E_ARG, "bgx_get_stats: null pointer");
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
-    unsigned long long st[8];
-    HIP_TRY(hipMemcpy(st, e->stats, sizeof(st), hipMemcpyDeviceToHost));
-    // decisions = records written, episodes = games finished: the lanes' own counters
-    const int L = e->cfg.lanes;
-    std::vector<uint32_t> rec(L), epi(L);
-    HIP_TRY(hipMemcpy(rec.data(), e->d.rec_count, (size_t)L * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(epi.data(), e->d.epi, (size_t)L * 4, hipMemcpyDeviceToHost));
-    unsigned long long dec = 0, eps = 0;
-    for (int i = 0; i < L; ++i) {
-        dec += rec[i];
-        eps += epi[i];
-    }
-    out->env_steps = st[0];
-    out->decisions = dec;
-    out->episodes = eps;
-    out->value_rows = st[3];
-    out->movegen_jobs = st[4];
-    out->fallback_jobs = st[5];
-    return BGX_OK;
+    return guarded("bgx_get_stats", [&]() -> int {
+        if (!e || !out) return fail(BGX_E_ARG, "bgx_get_stats: null pointer");
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+        unsigned long long st[8];
+        HIP_TRY(hipMemcpy(st, e->stats, sizeof(st), hipMemcpyDeviceToHost));
+        // decisions = records written, episodes = games finished: the lanes' own counters
+        const int L = e->cfg.lanes;
+        std::vector<uint32_t> rec(L), epi(L);
+        HIP_TRY(hipMemcpy(rec.data(), e->d.rec_count, (size_t)L * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(epi.data(), e->d.epi, (size_t)L * 4, hipMemcpyDeviceToHost));
+        unsigned long long dec = 0, eps = 0;
+        for (int i = 0; i < L; ++i) {
+            dec += rec[i];
+            eps += epi[i];
+        }
+        out->env_steps = st[0];
+        out->decisions = dec;
+        out->episodes = eps;
+        out->value_rows = st[3];
+        out->movegen_jobs = st[4];
+        out->fallback_jobs = st[5];
+        return BGX_OK;
+    });
 }
 
 int bgx_set_timing(bgx_engine* e, int enabled) {
-    if (!e) return fail(BGX_E_ARG, "bgx_set_timing: null engine");
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
-    for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
-    e->ev.clear();
-    e->ev_kind.clear();
-    e->ms_mg = e->ms_mlp = 0;
-    e->n_mg = e->n_mlp = 0;
-    e->timing = enabled != 0;
-    return BGX_OK;
+    return guarded("bgx_set_timing", [&]() -> int {
+        if (!e) return fail(BGX_E_ARG, "bgx_set_timing: null engine");
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+        for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+        e->ev.clear();
+        e->ev_kind.clear();
+        e->ms_mg = e->ms_mlp = 0;
+        e->n_mg = e->n_mlp = 0;
+        e->timing = enabled != 0;
+        return BGX_OK;
+    });
 }
 
 int bgx_get_timing(bgx_engine* e, double* ms_movegen, int* n_movegen, double* ms_mlp, int* n_mlp) {
-    if (!e) return fail(BGX_E_ARG, "bgx_get_timing: null engine");
-    HIP_TRY(hipSetDevice(e->device));
-    if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
-    for (size_t i = 0; i + 1 < e->ev.size(); i += 2) {
-        float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
-        if (e->ev_kind[i] == 0) { e->ms_mg += ms; e->n_mg++; }
-        else { e->ms_mlp += ms; e->n_mlp++; }
-    }
-    for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
-    e->ev.clear();
-    e->ev_kind.clear();
-    if (ms_movegen) *ms_movegen = e->ms_mg;
-    if (n_movegen) *n_movegen = e->n_mg;
-    if (ms_mlp) *ms_mlp = e->ms_mlp;
-    if (n_mlp) *n_mlp = e->n_mlp;
-    return BGX_OK;
+    return guarded("bgx_get_timing", [&]() -> int {
+        if (!e) return fail(BGX_E_ARG, "bgx_get_timing: null engine");
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+        for (size_t i = 0; i + 1 < e->ev.size(); i += 2) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, e->ev[i], e->ev[i + 1]));
+            if (e->ev_kind[i] == 0) { e->ms_mg += ms; e->n_mg++; }
+            else { e->ms_mlp += ms; e->n_mlp++; }
+        }
+        for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
+        e->ev.clear();
+        e->ev_kind.clear();
+        if (ms_movegen) *ms_movegen = e->ms_mg;
+        if (n_movegen) *n_movegen = e->n_mg;
+        if (ms_mlp) *ms_mlp = e->ms_mlp;
+        if (n_mlp) *n_mlp = e->n_mlp;
+        return BGX_OK;
+    });
 }
 
 }  // extern "C"

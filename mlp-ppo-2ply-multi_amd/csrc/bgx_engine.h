@@ -21,41 +21,36 @@ BGX_DEV uint64_t lane_key(uint64_t seed, uint32_t gid) {
     return z ^ (z >> 31);
 }
 
-struct LaneRng {
-    uint64_t key, ctr;
-    BGX_DEV u32x4 next() { return philox(key, 0x5EED0000ull, ctr++); }
-    BGX_DEV void roll(int& a, int& b) {
-        u32x4 r = next();
-        a = die_from(r.x);
-        b = die_from(r.y);
+// Dice streams. Normal mode: Philox4x32-10 keyed by (seed, global lane id),
+// one counter per draw. Scripted mode (test hook, bgx_engine_set_dice): the
+// lane's dice come from a table of single-die draws, consumed two per roll in
+// order (np.random.randint(1, 7) twice, backgammon_env.py:310-311), and the
+// counter is the table cursor; past the end a roll is (1, 2) and the engine
+// raises BGX_ERRF_DICE_EXHAUSTED. Scripted lanes play greedy (no uniform).
+struct DiceTab {
+    const uint8_t* tab = nullptr;   // the lane's row, or null
+    uint32_t len = 0;
+    BGX_DEV bool roll(uint64_t& ctr, int& a, int& b) const {   // false: past the end
+        const bool ok = ctr + 1 < (uint64_t)len;
+        a = ok ? (int)tab[ctr] : 1;
+        b = ok ? (int)tab[ctr + 1] : 2;
+        ctr += 2;
+        return ok;
     }
 };
 
-// The same stream drawn by a whole wavefront (one lane's game): lane k
-// evaluates Philox at counter base + k, so 64 draws cost one Philox
-// evaluation; draws come back by readlane (the counter is wave-uniform).
-struct WaveRng {
-    uint64_t key, ctr, base;
-    u32x4 batch;
-    BGX_DEV void refill() {
-        base = ctr;
-        batch = philox(key, 0x5EED0000ull, base + (uint64_t)lane_id());
-    }
-    BGX_DEV u32x4 at(int k) const {   // counter base + k, k < 64 (wave-uniform)
-        return {(uint32_t)__builtin_amdgcn_readlane((int)batch.x, k), (uint32_t)__builtin_amdgcn_readlane((int)batch.y, k),
-                (uint32_t)__builtin_amdgcn_readlane((int)batch.z, k), (uint32_t)__builtin_amdgcn_readlane((int)batch.w, k)};
-    }
-    BGX_DEV u32x4 next() {
-        if (ctr - base >= 64u) refill();
-        const u32x4 r = at((int)(ctr - base));
-        ++ctr;
-        return r;
-    }
+struct LaneRng {
+    uint64_t key, ctr;
+    DiceTab dt;
+    bool exhausted = false;
+    BGX_DEV u32x4 next() { return philox(key, 0x5EED0000ull, ctr++); }
     BGX_DEV void roll(int& a, int& b) {
+        if (dt.tab) { exhausted |= !dt.roll(ctr, a, b); return; }
         u32x4 r = next();
         a = die_from(r.x);
         b = die_from(r.y);
     }
+    BGX_DEV void skip_uniform() { if (!dt.tab) ++ctr; }
 };
 
 // The same stream drawn by a half-wave (two game lanes per wavefront, one
@@ -64,6 +59,8 @@ struct WaveRng {
 struct HalfRng {
     uint64_t key, ctr, base;
     u32x4 batch;
+    DiceTab dt;
+    bool exhausted = false;
     BGX_DEV void refill() {
         base = ctr;
         batch = philox(key, 0x5EED0000ull, base + (uint64_t)(lane_id() & 31));
@@ -80,10 +77,12 @@ struct HalfRng {
         return r;
     }
     BGX_DEV void roll(int& a, int& b) {
+        if (dt.tab) { exhausted |= !dt.roll(ctr, a, b); return; }
         u32x4 r = next();
         a = die_from(r.x);
         b = die_from(r.y);
     }
+    BGX_DEV void skip_uniform() { if (!dt.tab) ++ctr; }
 };
 
 // packed initial board (immutable_board.py:27-70): P1 {0:2, 11:5, 16:3, 18:5}, P2 {23:2, 12:5, 7:3, 5:5}
@@ -206,6 +205,16 @@ BGX_DEV void lane_store(const EngineDev& e, int i, const LaneState& s) {
     e.rng[i] = s.ctr;
 }
 
+// the lane's scripted dice (bgx_engine_set_dice), or none
+BGX_DEV DiceTab lane_dice(const EngineDev& e, int i) {
+    DiceTab d;
+    if (e.dice_tab) {
+        d.tab = e.dice_tab + (size_t)i * (size_t)e.dice_len;
+        d.len = (uint32_t)e.dice_len;
+    }
+    return d;
+}
+
 // One game lane's env step after its action is chosen (BackgammonEnv.step,
 // backgammon_env.py:130-221, + the worker's Experience, worker.py:101-162):
 // apply, judge, record, and on game end append the episode header and reset.
@@ -227,7 +236,7 @@ BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, Rng& rng, int
         rng.roll(s.d0, s.d1);
     } else {
         s.flags |= 16u << s.p;
-        rng.ctr++;   // the sampling uniform (lane_uniform)
+        rng.skip_uniform();   // the sampling uniform (lane_uniform)
         const int a = action;
         const int mover = s.p;
         const int dd0 = s.d0, dd1 = s.d1;
@@ -235,27 +244,23 @@ BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, Rng& rng, int
         done = o.done;
         if (done) { win_type = o.win_type; winner = mover; }
         else { s.p ^= 1; rng.roll(s.d0, s.d1); }
-        // experience record (worker.py:149-156; Experience, episode.py:5-46)
+        // experience record (worker.py:149-156; Experience, episode.py:5-46): the
+        // board before the move with the mover's indicator; the board after is
+        // the next record's before-board or the header's final board
         const uint32_t rec = s.rec;
         if (lead) {
             if (rec - s.harv >= (uint32_t)e.R) atomicOr(e.err_flags, BGX_ERRF_RING_OVERFLOW);
-            uint32_t* R = e.ring + ((size_t)i * e.R + (rec % (uint32_t)e.R)) * REC_WORDS;
-            uint32_t before[8];
-            for (int k = 0; k < 8; ++k) before[k] = s.w[k];
-            set_flag(before, mover);
-            uint32_t after[8];
-            for (int k = 0; k < 8; ++k) after[k] = nb[k];
-            set_flag(after, done ? mover : s.p);
-            store_packed(R, before);
-            store_packed(R + 8, after);
-            uint4 tail0 = make_uint4(__float_as_uint(vs), __float_as_uint(va), __float_as_uint(o.reward),
-                                     (uint32_t)a | ((uint32_t)(n_full > 0xFFFF ? 0xFFFF : n_full) << 16));
-            uint4 tail1 = make_uint4((uint32_t)dd0 | ((uint32_t)dd1 << 8) | ((uint32_t)o.done << 16) |
-                                         ((uint32_t)o.close << 17) | ((uint32_t)o.prime << 18) |
-                                         ((uint32_t)mover << 19) | ((uint32_t)o.win_type << 20),
-                                     s.epi, (uint32_t)s.steps, (uint32_t)(e.lane_base + i));
-            ((uint4*)(R + 16))[0] = tail0;
-            ((uint4*)(R + 16))[1] = tail1;
+            uint32_t* R = e.ring + ((size_t)i * e.R + (rec & (uint32_t)(e.R - 1))) * REC_WORDS;
+            const uint32_t w6 = (s.w[6] & 0xFFFFu) | ((uint32_t)mover << 16);
+            const uint32_t nm = (uint32_t)(n_full > 4095 ? 4095 : n_full);
+            const uint32_t st = (uint32_t)(s.steps > 511 ? 511 : s.steps);
+            ((uint4*)R)[0] = make_uint4(s.w[0], s.w[1], s.w[2], s.w[3]);
+            ((uint4*)R)[1] = make_uint4(s.w[4], s.w[5], w6, __float_as_uint(vs));
+            ((uint4*)R)[2] = make_uint4(__float_as_uint(va), __float_as_uint(o.reward),
+                                        (uint32_t)a | (nm << 11) | (st << 23),
+                                        (uint32_t)dd0 | ((uint32_t)dd1 << 3) | ((uint32_t)o.done << 6) |
+                                            ((uint32_t)o.close << 7) | ((uint32_t)o.prime << 8) |
+                                            ((uint32_t)mover << 9) | ((uint32_t)o.win_type << 10));
         }
         s.rec = rec + 1;
         for (int k = 0; k < 8; ++k) s.w[k] = nb[k];
@@ -272,7 +277,9 @@ BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, Rng& rng, int
                 ((uint4*)h)[1] = make_uint4((uint32_t)s.steps,
                                             (uint32_t)win_type | ((uint32_t)(winner & 0xFF) << 8) |
                                                 (s.flags << 16),
-                                            0u, 0u);
+                                            s.w[0], s.w[1]);
+                ((uint4*)h)[2] = make_uint4(s.w[2], s.w[3], s.w[4], s.w[5]);
+                ((uint4*)h)[3] = make_uint4(s.w[6], 0u, 0u, 0u);
             } else {
                 atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
             }
@@ -283,7 +290,10 @@ BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, Rng& rng, int
         s.epi = s.epi + 1;
         s.ep_first = s.rec;
     }
-    if (lead) store_packed(e.rows + (size_t)i * 8, s.w);
+    if (lead) {
+        store_packed(e.rows + (size_t)i * 8, s.w);
+        if (rng.exhausted) atomicOr(e.err_flags, BGX_ERRF_DICE_EXHAUSTED);
+    }
     s.ctr = rng.ctr;
 }
 
@@ -298,7 +308,10 @@ BGX_DEV void step_lane(const EngineDev& e, int i, int action) {
     lane_load(e, i, s);
     uint32_t nb[8];
     load_packed(e.rows + (size_t)(base + (act ? action : 0)) * 8, nb);
-    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), s.ctr};
+    LaneRng rng;
+    rng.key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
+    rng.ctr = s.ctr;
+    rng.dt = lane_dice(e, i);
     lane_advance(e, i, s, rng, action, nb, e.V[i], act ? e.V[base + action] : 0.0f, n_full, true);
     lane_store(e, i, s);
 }

@@ -21,10 +21,14 @@ namespace bgx {
 __global__ __launch_bounds__(256) void engine_reset_kernel(EngineDev e) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.L) return;
-    LaneRng rng = {lane_key(e.seed, (uint32_t)(e.lane_base + i)), 0};
+    LaneRng rng;
+    rng.key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
+    rng.ctr = 0;
+    rng.dt = lane_dice(e, i);
     uint32_t w[8];
     int d0, d1;
     const int p = new_game(rng, w, d0, d1);
+    if (rng.exhausted) atomicOr(e.err_flags, BGX_ERRF_DICE_EXHAUSTED);
     store_packed(e.rows + (size_t)i * 8, w);
     e.player[i] = (uint8_t)p;
     e.dice[2 * i] = (uint8_t)d0;
@@ -269,7 +273,6 @@ __global__ __launch_bounds__(256) void two_ply_reduce_kernel(const float* __rest
     out[i] = W;
 }
 
-// harvest: copy finished episodes' records out of the lane rings
 // harvest, step 1 (one workgroup): record offsets of the finished episodes
 // (exclusive scan of their record counts) and the harvest totals, read on the
 // device so the host needs one small copy: info = {episodes, records, error
@@ -306,25 +309,32 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
         info[3] = n_raw;
         *e.ep_count = 0u;
     }
+    // every finished episode is harvested now (the list holds them all: ep_cap
+    // is sized for the steps a ring allows between harvests), so a lane's
+    // unharvested records start at its current episode: harv = ep_first (a
+    // plain store, wrap-safe for the 32-bit record counters)
+    for (int i = t; i < e.L; i += 1024) e.harv[i] = e.ep_first[i];
 }
 
-// harvest, step 2: copy finished episodes' records out of the lane rings
-// (persistent grid; the episode count comes from harvest_scan_kernel)
+// harvest, step 2: copy finished episodes' records out of the lane rings,
+// 16 bytes per thread (a record is three uint4; persistent grid; the episode
+// count comes from harvest_scan_kernel)
 __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
                                                      const int32_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ info, uint32_t* __restrict__ out) {
     const int n_eps = (int)info[0];
+    constexpr int Q = REC_WORDS / 4;
     for (int ep = blockIdx.x; ep < n_eps; ep += gridDim.x) {
         const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
         const int lane = (int)h[0] - e.lane_base;
         const uint32_t first = h[2], nrec = h[3];
-        const size_t words = (size_t)nrec * REC_WORDS;
-        for (size_t q = threadIdx.x; q < words; q += blockDim.x) {
-            const uint32_t r = (uint32_t)(q / REC_WORDS), k = (uint32_t)(q % REC_WORDS);
-            const uint32_t slot = (first + r) % (uint32_t)e.R;
-            out[((size_t)offs[ep] + r) * REC_WORDS + k] = e.ring[((size_t)lane * e.R + slot) * REC_WORDS + k];
+        const uint4* src = (const uint4*)(e.ring + (size_t)lane * e.R * REC_WORDS);
+        uint4* dst = (uint4*)(out + (size_t)offs[ep] * REC_WORDS);
+        for (uint32_t q = threadIdx.x; q < nrec * Q; q += blockDim.x) {
+            const uint32_t r = q / Q, k = q - r * Q;
+            const uint32_t slot = (first + r) & (uint32_t)(e.R - 1);
+            dst[q] = src[slot * Q + k];
         }
-        if (threadIdx.x == 0) atomicMax(e.harv + lane, first + nrec);
     }
 }
 

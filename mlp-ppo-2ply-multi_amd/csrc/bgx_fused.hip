@@ -285,6 +285,7 @@ __global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
                 HalfRng rng;
                 rng.key = lane_key(e.seed, (uint32_t)(e.lane_base + i));
                 rng.ctr = sr.ctr;
+                rng.dt = lane_dice(e, i);
                 rng.refill();
                 if (n <= 0) {
                     lane_advance(e, i, sr, rng, -1, sr.w, 0.0f, 0.0f, 0, lead);

@@ -8,6 +8,7 @@
 #define BGX_ERRF_FALLBACK_OVERFLOW 4u   // a job outgrew the global workspace
 #define BGX_ERRF_RING_OVERFLOW 8u       // experience ring overwritten before harvest
 #define BGX_ERRF_EPISODE_LIST 16u       // finished-episode list full
+#define BGX_ERRF_DICE_EXHAUSTED 32u     // a lane read past its scripted dice (bgx_engine_set_dice)
 
 namespace bgx {
 
@@ -47,7 +48,8 @@ struct MovegenArgs {
     size_t ws_words_per_wave;    // >= 5 * ws_slots
     int ovf_zeroed;              // caller zeroed *ovf_count on the stream already (skip the memset)
     int heavy_t;                 // set by the launcher: doubles level size handed to the block tier
-    int exp_mode;                // development only (BGX_MG_EXP): 1 skip emission, 2 skip dedup
+    int force_table;             // test hook (BGX_MG_TEST_TABLE=1): every job takes the hash-table path
+                                 //   (no table-free doubles / non-doubles rules), as a cross-check
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
     unsigned* err_flags;
 };
@@ -67,8 +69,16 @@ struct MlpArgs {
 };
 
 // Self-play lane state (one engine per device), structure of arrays.
-constexpr int REC_WORDS = 24;   // experience record: 96 B
-constexpr int EP_WORDS = 8;     // episode header: 32 B
+// Experience record (48 B; include/bgx.h bgx_harvest): words 0..6 the packed
+// board before the move (word 6 bit 16 = the mover), 7 V(s), 8 V(a), 9 reward,
+// 10 action | n_moves << 11 | step << 23, 11 dice0 | dice1 << 3 | done << 6 |
+// close_out << 7 | prime << 8 | mover << 9 | win_type << 10. The board after
+// the move is the next record's before-board (passes do not move checkers), or
+// for an episode's last record the final board in its header.
+constexpr int REC_WORDS = 12;
+// Episode header (64 B): global lane, episode no., first record, n_records,
+// env steps, win_type | winner << 8 | flags << 16, final board words 0..6, 0, 0, 0
+constexpr int EP_WORDS = 16;
 
 struct EngineDev {
     int L;                       // lanes on this engine
@@ -93,7 +103,9 @@ struct EngineDev {
     uint32_t* ep_first;          // [L] first record of the current episode
     uint32_t* harv;              // [L] records harvested (absolute)
     uint32_t* ring;              // [L][R][REC_WORDS]
-    int R;
+    int R;                       // ring slots per lane (a power of two: slot = record counter & (R - 1))
+    const uint8_t* dice_tab;     // test hook (bgx_engine_set_dice): [L][dice_len] scripted single-die draws, or null
+    int dice_len;
     uint32_t* ep_list;           // [ep_cap][EP_WORDS]
     unsigned* ep_count;
     int ep_cap;
@@ -131,7 +143,6 @@ struct FusedArgs {
     size_t ws_words_per_block;
     int force_tier;              // test hook (BGX_MG_TEST_TIER)
     unsigned long long* prof;    // development (BGX_FUSED_PROF): [gridDim.x][16] phase clocks, or null
-    int exp;                     // development (BGX_FUSED_EXP): variant bits
 };
 
 }  // namespace bgx

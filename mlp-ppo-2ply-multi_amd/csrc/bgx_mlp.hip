@@ -168,10 +168,9 @@ BGX_DEV void epi_pair(const floatx16& acc, int m, int r0, int h, const float* w2
     v = fmaf(c.y, __builtin_amdgcn_rcpf(1.0f + e1), v);
 }
 
-// PREF: the next tile pair's rows are loaded while this pair's MFMAs run.
-// SKIP: k-steps whose B fragment is zero on every board of the pair skip
-// their MFMAs (tile_kmask; exact, V keeps its bits).
-template <bool PREF, bool SKIP>
+// (Measured and rejected on the 2-ply reply launch, DESIGN.md §4: loading the
+// next tile pair's rows during this pair's MFMAs, and skipping all-zero
+// k-steps -- the branches break the MFMA / epilogue interleave.)
 __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
     constexpr int NT = 2;
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
@@ -193,36 +192,19 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
     const int NW = blockDim.x >> 6;
     const int nwaves = gridDim.x * NW;
     int t = blockIdx.x * NW + wave;
-    uint4 px[NT], py[NT];
-    if (PREF) {
-#pragma unroll
-        for (int q = 0; q < NT; ++q) load_rows(a, n, t * NT + q, NT, col, px[q], py[q]);
-    }
     __syncthreads();
     for (; t < tiles; t += nwaves) {
         // k-steps 0..11 from the LUT, kept in registers; k-step 12 (bars, borne-off,
         // side to move, bias) is rebuilt from the row word per hidden tile
         half8 b[KSTEPS - 1][NT];
         uint32_t w6[NT];
-        uint32_t km = 1u << (KSTEPS - 1);
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
             uint4 bx, by;
-            if (PREF) {
-                bx = px[q];
-                by = py[q];
-            } else {
-                load_rows(a, n, t * NT + q, NT, col, bx, by);
-            }
+            load_rows(a, n, t * NT + q, NT, col, bx, by);
 #pragma unroll
             for (int s = 0; s < KSTEPS - 1; ++s) b[s][q] = feat_frag(bx, by, s, h, lut, a.feat_scale);
             w6[q] = by.z;
-            if (SKIP) km |= tile_kmask(bx, by);
-        }
-        if (!SKIP) km = (1u << KSTEPS) - 1u;
-        if (PREF) {
-#pragma unroll
-            for (int q = 0; q < NT; ++q) load_rows(a, n, (t + nwaves) * NT + q, NT, col, px[q], py[q]);
         }
         float v[NT] = {0.0f, 0.0f}, pm[NT] = {0.0f, 0.0f};   // canonical epilogue order (bgx_mlp.h)
         floatx16 acc[2][NT];
@@ -242,17 +224,13 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
                 const int sn = s + 1 < KSTEPS ? s + 1 : 0;
                 const uint4 nh = wf[((0 * 4 + mn) * KSTEPS + sn) * 64 + lane];
                 const uint4 nl = wf[((1 * 4 + mn) * KSTEPS + sn) * 64 + lane];
-                if (km & (1u << s)) {
 #pragma unroll
-                    for (int q = 0; q < NT; ++q) {
-                        const half8 bq = s < KSTEPS - 1 ? b[s < KSTEPS - 1 ? s : 0][q]
-                                                        : feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, w6[q], 0),
-                                                                    KSTEPS - 1, h, lut, a.feat_scale);
-                        acc[cur][q] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, bq, acc[cur][q], 0, 0, 0);
-                        acc[cur][q] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, bq, acc[cur][q], 0, 0, 0);
-                    }
+                for (int q = 0; q < NT; ++q) {
+                    const half8 bq = s < KSTEPS - 1 ? b[s < KSTEPS - 1 ? s : 0][q]
+                                                    : feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, w6[q], 0),
+                                                                KSTEPS - 1, h, lut, a.feat_scale);
+                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, bq, acc[cur][q], 0, 0, 0);
+                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, bq, acc[cur][q], 0, 0, 0);
                 }
                 // tile m-1's epilogue, spread over k-steps 0..7 (2 rows per step per board tile)
                 if (m > 0 && s < 8) {
@@ -334,35 +312,13 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
             n_cu = 256;
         if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel<2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il<false, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il<true, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il<false, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il<true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+                hipSuccess)
             return hipErrorInvalidValue;
     }
-    // throughput kernel variants (BGX_MLP_PREF / BGX_MLP_SKIP = 1: on). Both
-    // off by default: measured on the 2-ply K=4 reply launch (profiles/r1e),
-    // the prefetch 0.219 -> 0.227 ms and prefetch + skip 0.312 ms (the
-    // skip's branches break the MFMA / epilogue interleave)
-    static int pref = -1, skip = -1;
-    if (pref < 0) {
-        const char* v = getenv("BGX_MLP_PREF");
-        pref = v ? atoi(v) : 0;
-        v = getenv("BGX_MLP_SKIP");
-        skip = v ? atoi(v) : 0;
-    }
-    static int nt_override = -1;
-    if (nt_override < 0) {
-        const char* v = getenv("BGX_MLP_NT");
-        nt_override = v ? atoi(v) : 0;
-    }
-    const int nt = (nt_override ? nt_override : args->nt) == 2 ? 2 : 1;
+    // nt = 1: latency-bound small batches (one 32-board tile per wave, 16-wave
+    // blocks); nt = 2: throughput (the interleaved-epilogue kernel, 8 waves)
+    const int nt = args->nt == 2 ? 2 : 1;
     const int nw = nt == 2 ? 8 : 16;
     int blocks = n_cu;
     if (!args->n_rows_dev) {
@@ -371,21 +327,8 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
         if (need < blocks) blocks = need;
         if (blocks <= 0) return hipSuccess;
     }
-    static int il = -1;
-    if (il < 0) {
-        const char* v = getenv("BGX_MLP_IL");
-        il = v ? atoi(v) : 1;
-    }
-    if (nt == 2 && il && pref && skip)
-        hipLaunchKernelGGL((bgx::mlp_kernel_il<true, true>), dim3(blocks), dim3(512), lds, stream, *args);
-    else if (nt == 2 && il && pref)
-        hipLaunchKernelGGL((bgx::mlp_kernel_il<true, false>), dim3(blocks), dim3(512), lds, stream, *args);
-    else if (nt == 2 && il && skip)
-        hipLaunchKernelGGL((bgx::mlp_kernel_il<false, true>), dim3(blocks), dim3(512), lds, stream, *args);
-    else if (nt == 2 && il)
-        hipLaunchKernelGGL((bgx::mlp_kernel_il<false, false>), dim3(blocks), dim3(512), lds, stream, *args);
-    else if (nt == 2)
-        hipLaunchKernelGGL((bgx::mlp_kernel<2, 8>), dim3(blocks), dim3(512), lds, stream, *args);
+    if (nt == 2)
+        hipLaunchKernelGGL(bgx::mlp_kernel_il, dim3(blocks), dim3(512), lds, stream, *args);
     else
         hipLaunchKernelGGL((bgx::mlp_kernel<1, 16>), dim3(blocks), dim3(1024), lds, stream, *args);
     return hipGetLastError();

@@ -28,7 +28,7 @@ struct Mem {
     uint32_t* fb;              // [F]
     uint32_t* map;             // [64] parent start marks for one child chunk (kept zero between uses)
     int S, F;
-    int exp = 0;               // development experiments (MovegenArgs::exp_mode)
+    int force_table = 0;       // test hook (MovegenArgs::force_table): hash-table path for every job
 };
 
 // LDS (wavefront scope) or global (agent scope) accessors
@@ -528,13 +528,11 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
         const uint32_t key = kfn(p, s);
         const uint32_t ord = ord_base + (uint32_t)r;
         bool fresh;
-        uint32_t slot = 0;
-        if (M.exp & 2) fresh = act;
-        else slot = dedup_insert<G>(M, act, key, ord, fresh);
+        const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
         inserted += __popcll(ballot(fresh));
         if (inserted > M.S - (M.S >> 2) || n_out + 64 > M.F) return false;
         sync<G>();
-        const bool sv = act && ((M.exp & 2) ? true : (uint32_t)ld64<G>(M.tab + slot) == ord);
+        const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
         const uint64_t bm = ballot(sv);
         if (sv) st32<G>(out + n_out + mask_prefix(bm), key | tag);
         n_out += __popcll(bm);
@@ -609,7 +607,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         const int nH = mH.n, nL = mL.n;
         const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
         const bool h1 = v1 && t1 < 24u && ((R.blot >> t1) & 1u);
-        if ((two1 || (nH != 1 && two2)) && nd_by_rule(R) && !(M.exp & 4)) {
+        if ((two1 || (nH != 1 && two2)) && nd_by_rule(R) && !M.force_table) {
             // 2-move records without a table (nd_first): a pass-2 parent can
             // only add its chain (s2 = t1) or reverse chain (s2 -> s1) child
             if (pass == 1) {
@@ -672,7 +670,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         const uint32_t okd = ok_mask(R.block, d, R.player);
         uint32_t* fa = M.fa;
         uint32_t* fb = M.fb;
-        if (doubles_by_path(R)) {
+        if (doubles_by_path(R) && !M.force_table) {
             if (l == 0) st32<G>(fa, PATH_EMPTY);
             sync<G>();
             int n = 1, level = 0;
@@ -810,7 +808,7 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
     const int nfin = job_records<G>(in, M, fin, heavy_t);
     if (nfin < 0) return nfin;
     const int base = begin_emit(a, j, nfin, fc);
-    if (base >= 0 && !(M.exp & 1)) emit_records<G>(a, j, in, fin, nfin, base);
+    if (base >= 0) emit_records<G>(a, j, in, fin, nfin, base);
     return nfin;
 }
 
@@ -941,8 +939,8 @@ BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
 }
 
 // returns the record count (records in `fin`), -1 = overflow (tier 3)
-BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin) {
-    if (doubles_by_path(in.R)) return coop_doubles_path(in, C, fin);
+BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin, bool force_table = false) {
+    if (doubles_by_path(in.R) && !force_table) return coop_doubles_path(in, C, fin);
     const Root& R = in.R;
     const int d = in.d0;
     const int t = (int)threadIdx.x, l = lane_id();

@@ -36,43 +36,20 @@
 
 namespace bgx {
 
-// Tier 1, persistent: wave w walks jobs w, w + gridDim.x, ... Launches with
-// no more jobs than resident waves (latency-bound) also hand doubles jobs with
-// a level over HEAVY_T children to tier 2, where a block expands them.
-template <int S>
-__global__ __launch_bounds__(64) void movegen_lds_kernel(MovegenArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned long long smem[Slice<S>::bytes / 8];
-    Mem M = lds_mem<S>(smem);
-    M.exp = a.exp_mode;
-    const int n_jobs = uniform(job_count(a));
-    FlatCursor fc;
-    for (int j = (int)blockIdx.x; j < n_jobs; j += (int)gridDim.x) {
-        const JobIn in = fetch_job(a, j);
-        if (in.skip) {
-            begin_emit(a, j, 0, fc);
-            continue;
-        }
-        const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc, a.heavy_t);
-        if (r < 0 && lane_id() == 0) push_ovf(a, j);   // overflow (-1) or heavy doubles (-2)
-    }
-}
-
 // Tier 1 for large launches (the 2-ply replies), balanced: a workgroup of PW
 // waves owns the interleaved jobs b, b + G, ... and its waves take the next
 // one from an LDS counter. With a static per-wave stride the launch lasts as
 // long as its unluckiest wave (67 jobs of very different cost each for the
 // 344 k reply jobs of a 4,096-lane K=4 step); here a wave that drew cheap jobs
 // takes more. The next job's board is loaded while the current job runs.
-// PW waves per workgroup: 10 (two workgroups per CU, the default) or 5 (four)
+// PW = 10 waves per workgroup, two workgroups per CU (measured against four
+// 5-wave workgroups: within run noise)
 constexpr int PW = 10;
 constexpr int PF = Slice<S_T1>::F - 8;                  // frontier entries: PW slices + the counter fit
 constexpr int PSL = S_T1 * 8 + 2 * PF * 4 + 64 * 4;     // slice bytes
 static_assert(PW * PSL + 16 <= 80 * 1024, "two 10-wave workgroups per CU");
-static_assert(5 * PSL + 16 <= 40 * 1024, "four 5-wave workgroups per CU");
 
-template <int NWP>
-__global__ __launch_bounds__(64 * NWP) void movegen_pool_kernel(MovegenArgs a) {
-    constexpr int PW = NWP;
+__global__ __launch_bounds__(64 * PW) void movegen_pool_kernel(MovegenArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
     __shared__ int next_job;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
@@ -84,7 +61,7 @@ __global__ __launch_bounds__(64 * NWP) void movegen_pool_kernel(MovegenArgs a) {
     M.fa = (uint32_t*)(sl + S_T1);
     M.fb = M.fa + PF;
     M.map = M.fb + PF;
-    M.exp = a.exp_mode;
+    M.force_table = a.force_table;
     M.map[l] = 0u;
     const int n_jobs = uniform(job_count(a));
     // the workgroup's jobs are b, b + G, b + 2G, ... (a contiguous range would
@@ -135,6 +112,7 @@ __global__ __launch_bounds__(NTH) void movegen_few_kernel(MovegenArgs a) {
     M.fb = M.fa + M.F;
     M.map = M.fb + M.F;
     M.S = S_T1;
+    M.force_table = a.force_table;
     M.map[l] = 0u;
     for (int win = (int)blockIdx.x; win * BW < n_jobs; win += (int)gridDim.x) {
         const int j = win * BW + w;
@@ -215,6 +193,7 @@ __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
         G.map = base + 4 * S;
         G.S = S;
         G.F = S;
+        G.force_table = a.force_table;
         st32<true>(G.map + l, 0u);
         sync<true>();
         if (run_job<true>(a, j, in, G, fc) < 0 && l == 0) atomicOr(a.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
@@ -225,7 +204,8 @@ __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
         if (in.d0 != in.d1 || a.force_tier >= 3) {
             if (w == 0) {
                 static_assert(Slice<S_T2>::bytes <= sizeof(CoopLds), "slice fits");
-                const Mem M = lds_mem<S_T2>(smem);
+                Mem M = lds_mem<S_T2>(smem);
+                M.force_table = a.force_table;
                 const int r = a.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M, fc);
                 if (r < 0) run_global(j, in);
             }
@@ -233,7 +213,7 @@ __global__ __launch_bounds__(NTH) void movegen_block_kernel(MovegenArgs a) {
             continue;
         }
         uint32_t* fin = nullptr;
-        const int nfin = coop_doubles(in, C, fin);
+        const int nfin = coop_doubles(in, C, fin, a.force_table != 0);
         if (nfin < 0) {
             if (w == 0) run_global(j, in);
             __syncthreads();
@@ -275,60 +255,43 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         if (e != hipSuccess) return e;
     }
     // resident blocks per CU of each kernel (LDS, registers, 32 waves)
-    static int per_cu1 = 0, per_cub = 0, per_cuf = 0, per_cup = 0, per_cup5 = 0;
-    if (!per_cu1) {
+    static int per_cub = 0, per_cuf = 0, per_cup = 0;
+    if (!per_cub) {
         auto occ = [](int& n, const void* k, int threads, int dflt) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n <= 0) n = dflt;
         };
-        occ(per_cu1, (const void*)bgx::movegen_lds_kernel<bgx::S_T1>, 64, 20);
-        occ(per_cup, (const void*)bgx::movegen_pool_kernel<bgx::PW>, 64 * bgx::PW, 2);
-        occ(per_cup5, (const void*)bgx::movegen_pool_kernel<5>, 64 * 5, 4);
+        occ(per_cup, (const void*)bgx::movegen_pool_kernel, 64 * bgx::PW, 2);
         occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
         occ(per_cuf, (const void*)bgx::movegen_few_kernel, bgx::NTH, 1);
     }
-    // test hook: route every job to tier 2 (2) or tier 3 (3)
-    if (const char* v = getenv("BGX_MG_TEST_TIER")) a.force_tier = atoi(v);
-    if (const char* v = getenv("BGX_MG_EXP")) a.exp_mode = atoi(v);   // development only
-    int coop = -1;
-    if (const char* v = getenv("BGX_MG_COOP")) coop = atoi(v);
+    // test hooks (parity cross-checks; three getenv per launch, next to a
+    // kernel launch's cost): BGX_MG_TEST_TIER=2/3 routes every job to tier 2 / 3;
+    // BGX_MG_TEST_TABLE=1 sends every job down the hash-table path; BGX_MG_FEW=0/1
+    // forces the tier-1 kernel choice below (the two kernels give identical rows)
+    const char* ev = getenv("BGX_MG_TEST_TIER");
+    const int test_tier = ev ? atoi(ev) : 0;
+    ev = getenv("BGX_MG_TEST_TABLE");
+    const int test_table = ev ? atoi(ev) : 0;
+    ev = getenv("BGX_MG_FEW");
+    const int fewm = ev ? atoi(ev) : -1;
+    a.force_tier = test_tier;
+    a.force_table = test_table;
+    // doubles run table-free in tier 1 (the block-cooperative hand-off of heavy
+    // doubles measured slower since then: DESIGN.md §4)
+    a.heavy_t = 0x7FFFFFFF;
     // latency-bound launches (at most 4 windows of 16 jobs per CU, host-known
-    // count): tier 1 in 16-wave blocks with one flat-row atomic per block
-    // (BGX_MG_FEW=0/1 forces the per-wave / per-block kernel)
-    int fewm = -1;
-    if (const char* v = getenv("BGX_MG_FEW")) fewm = atoi(v);
+    // count): tier 1 in 16-wave blocks with one flat-row atomic per block;
+    // larger launches: the balanced pool kernel
     const bool few_jobs = !a.n_jobs_dev && a.n_jobs <= n_cu * per_cuf * bgx::BW * 4;
-    const bool few = fewm == 1 || (fewm < 0 && few_jobs);
-    // large launches: the balanced pool kernel (BGX_MG_POOL=0: the strided per-wave kernel)
-    int poolm = 1;
-    if (const char* v = getenv("BGX_MG_POOL")) poolm = atoi(v);
-    const bool pool = poolm != 0;
-    int heavy = bgx::HEAVY_T;
-    if (const char* v = getenv("BGX_MG_HEAVY_T")) heavy = atoi(v);
-    // heavy doubles go to the block-cooperative tier 2 when the launch is
-    // latency-bound (BGX_MG_COOP=1/0 forces it on/off)
-    // heavy-doubles hand-off to tier 2: off by default since doubles outside
-    // bear-off expand table-free in tier 1 (measured 1-ply: off 66-67 M env
-    // steps/s, thresholds 32 / 64 / 128 / 256: 53 / 61-64 / 60 / 57 M)
-    (void)few_jobs;
-    a.heavy_t = coop == 1 ? heavy : 0x7FFFFFFF;
-    if (few) {
+    if (fewm == 1 || (fewm < 0 && few_jobs)) {
         int blocks = a.n_jobs_dev ? n_cu * per_cuf : (a.n_jobs + bgx::BW - 1) / bgx::BW;
         if (blocks > n_cu * per_cuf) blocks = n_cu * per_cuf;
         hipLaunchKernelGGL(bgx::movegen_few_kernel, dim3(blocks), dim3(bgx::NTH), 0, stream, a);
-    } else if (pool) {
-        // balanced tier 1: 10-wave workgroups over contiguous job ranges
-        const int pw = poolm == 5 ? 5 : bgx::PW;   // BGX_MG_POOL=5: four 5-wave workgroups per CU
-        int blocks = n_cu * (pw == 5 ? per_cup5 : per_cup);
-        const int need = (a.n_jobs + pw - 1) / pw;
-        if (!a.n_jobs_dev && need < blocks) blocks = need;
-        if (pw == 5)
-            hipLaunchKernelGGL(bgx::movegen_pool_kernel<5>, dim3(blocks), dim3(64 * 5), 0, stream, a);
-        else
-            hipLaunchKernelGGL(bgx::movegen_pool_kernel<bgx::PW>, dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
     } else {
-        int blocks = n_cu * per_cu1;
-        if (!a.n_jobs_dev && a.n_jobs < blocks) blocks = a.n_jobs;
-        hipLaunchKernelGGL(bgx::movegen_lds_kernel<bgx::S_T1>, dim3(blocks), dim3(64), 0, stream, a);
+        int blocks = n_cu * per_cup;
+        const int need = (a.n_jobs + bgx::PW - 1) / bgx::PW;
+        if (!a.n_jobs_dev && need < blocks) blocks = need;
+        hipLaunchKernelGGL(bgx::movegen_pool_kernel, dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -24,7 +24,7 @@ import numpy as np
 
 from .shm_ring import ShmRing
 
-EP_WORDS, REC_WORDS = 8, 24
+from bgx.records import EP_WORDS, REC_WORDS  # noqa: E402  (the engine's wire format)
 
 
 def pack_message(headers: np.ndarray, records: np.ndarray) -> bytes:
@@ -90,7 +90,7 @@ class ExperienceQueue:
 
     # --- bulk path
     def put_records(self, headers, records, timeout=None) -> bool:
-        """One harvest (host arrays: headers [n, 8], records [m, 24] uint32, the
+        """One harvest (host arrays: headers [n, 16], records [m, 12] uint32, the
         episodes' records contiguous in header order) as one ring message."""
         h = np.asarray(headers)
         return self.ring.put(pack_message(h, records), n_episodes=int(h.shape[0]), timeout=timeout)

@@ -70,7 +70,7 @@ class Worker:
 
     def harvest_records(self, steps=None):
         """Advance all lanes; return the finished episodes as compact host arrays
-        (headers uint32 [n, 8], records uint32 [m, 24]) for the bulk queue path."""
+        (headers uint32 [n, 16], records uint32 [m, 12]) for the bulk queue path."""
         eng = self._ensure_engine()
         eng.step(steps or self.steps_per_harvest)
         h = eng.harvest()

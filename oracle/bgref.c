@@ -671,7 +671,47 @@ typedef struct {
     int tid;
     double seconds;
     long long steps, decisions, episodes;
+    int ply;          /* 1: softmax(V/T) over every candidate (worker.py:137-143);
+                         2: two_ply.py:44-90 scoring of the top-4 by V, softmax over the four */
 } sp_arg;
+
+/* compute_weighted_opponent_response (two_ply.py:93-150), exact mode, in
+ * fp32 batches (the CPU port's arithmetic, like bgref_value_f32) */
+static double two_ply_response_f32(const uint8_t* board, int opp, const sp_arg* a, float* x, float* v) {
+    double total = 0.0;
+    for (int r = 0; r < 21; ++r) {
+        full_t* fm;
+        int n = all_moves(board, opp, DICE_ROLLS[r][0], DICE_ROLLS[r][1], &fm);
+        if (n > 0) {
+            uint8_t nb[52];
+            int done = 0;
+            double top[5];
+            int nt = 0;
+            while (done < n) {   /* batches of up to 500 replies */
+                const int b = n - done < 500 ? n - done : 500;
+                for (int i = 0; i < b; ++i) {
+                    execute_full_move(board, opp, &fm[done + i], nb);
+                    bgref_encode(nb, opp, 0, x + (size_t)i * BGREF_NFEAT);
+                }
+                bgref_value_f32(a->W1, a->b1, a->w2, a->b2, x, b, v);
+                for (int i = 0; i < b; ++i) {   /* running top 5, descending */
+                    double y = v[i];
+                    int k = nt < 5 ? nt++ : 5;
+                    if (k == 5 && y <= top[4]) continue;
+                    if (k == 5) k = 4;
+                    while (k > 0 && top[k - 1] < y) { top[k] = top[k - 1]; --k; }
+                    top[k] = y;
+                }
+                done += b;
+            }
+            double s = 0.0;
+            for (int i = 0; i < nt; ++i) s += top[i];
+            total += (s / nt) * ((double)COUNTS[r] / 36.0);
+        }
+        free(fm);
+    }
+    return total;
+}
 
 typedef struct {
     uint64_t key;
@@ -701,6 +741,8 @@ static void* sp_thread(void* p) {
     float* x = (float*)malloc(sizeof(float) * 501 * BGREF_NFEAT);
     float* v = (float*)malloc(sizeof(float) * 501);
     double* pr = (double*)malloc(sizeof(double) * 501);
+    float* x2 = (float*)malloc(sizeof(float) * 500 * BGREF_NFEAT);
+    float* v2 = (float*)malloc(sizeof(float) * 500);
     double t0 = now_s();
     long long steps = 0, dec = 0, eps = 0;
     while (now_s() - t0 < a->seconds) {
@@ -731,12 +773,30 @@ static void* sp_thread(void* p) {
             }
             free(fm);
             bgref_value_f32(a->W1, a->b1, a->w2, a->b2, x, n + 1, v);
+            /* scores: 1-ply V, or (2-ply, >= 4 moves) alpha*V - beta*W of the top 4 by V */
+            int cand[500], m = n;
+            double sc[500];
+            for (int i = 0; i < n; ++i) { cand[i] = i; sc[i] = v[i + 1]; }
+            if (a->ply == 2 && n >= 4) {
+                for (int c = 0; c < 4; ++c) {   /* top-4 by V, ties to the lower index */
+                    int best = c;
+                    for (int i = c + 1; i < n; ++i)
+                        if (v[cand[i] + 1] > v[cand[best] + 1] ||
+                            (v[cand[i] + 1] == v[cand[best] + 1] && cand[i] < cand[best])) best = i;
+                    int t = cand[c]; cand[c] = cand[best]; cand[best] = t;
+                }
+                m = 4;
+                for (int c = 0; c < 4; ++c)
+                    sc[c] = 1.0 * v[cand[c] + 1] -
+                            0.9 * two_ply_response_f32(legal + (size_t)cand[c] * 52, 1 - pl, a, x2, v2);
+            }
             double mx = -1e300, s = 0.0;
-            for (int i = 0; i < n; ++i) if (v[i + 1] / a->temperature > mx) mx = v[i + 1] / a->temperature;
-            for (int i = 0; i < n; ++i) { pr[i] = exp(v[i + 1] / a->temperature - mx); s += pr[i]; }
+            for (int i = 0; i < m; ++i) if (sc[i] / a->temperature > mx) mx = sc[i] / a->temperature;
+            for (int i = 0; i < m; ++i) { pr[i] = exp(sc[i] / a->temperature - mx); s += pr[i]; }
             double u = (rng_u32(&rng) >> 8) * (1.0 / 16777216.0) * s;
-            int act = n - 1;
-            for (int i = 0; i < n; ++i) { u -= pr[i]; if (u < 0) { act = i; break; } }
+            int act = m - 1;
+            for (int i = 0; i < m; ++i) { u -= pr[i]; if (u < 0) { act = i; break; } }
+            act = cand[act];
             memcpy(board, legal + (size_t)act * 52, 52);
             if (bgref_check_game_over(board, pl)) {
                 (void)bgref_check_for_backgammon(board, pl);
@@ -756,7 +816,7 @@ static void* sp_thread(void* p) {
     a->steps = steps;
     a->decisions = dec;
     a->episodes = eps;
-    free(legal); free(x); free(v); free(pr);
+    free(legal); free(x); free(v); free(pr); free(x2); free(v2);
     return NULL;
 }
 
@@ -764,12 +824,20 @@ long long bgref_selfplay_bench(const float* W1, const float* b1, const float* w2
                                const float* b2, float temperature, uint64_t seed,
                                int n_threads, double seconds, long long* decisions,
                                long long* episodes, double* elapsed) {
+    return bgref_selfplay_bench_ply(W1, b1, w2, b2, temperature, seed, n_threads, seconds, 1,
+                                    decisions, episodes, elapsed);
+}
+
+long long bgref_selfplay_bench_ply(const float* W1, const float* b1, const float* w2,
+                                   const float* b2, float temperature, uint64_t seed,
+                                   int n_threads, double seconds, int ply, long long* decisions,
+                                   long long* episodes, double* elapsed) {
     if (n_threads < 1) n_threads = 1;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * n_threads);
     sp_arg* args = (sp_arg*)calloc(n_threads, sizeof(sp_arg));
     double t0 = now_s();
     for (int i = 0; i < n_threads; ++i) {
-        args[i] = (sp_arg){W1, b1, w2, b2, temperature, seed, i, seconds, 0, 0, 0};
+        args[i] = (sp_arg){W1, b1, w2, b2, temperature, seed, i, seconds, 0, 0, 0, ply};
         pthread_create(&th[i], NULL, sp_thread, &args[i]);
     }
     long long s = 0, d = 0, e = 0;

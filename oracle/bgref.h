@@ -120,6 +120,15 @@ long long bgref_selfplay_bench(const float* W1, const float* b1, const float* w2
                                long long* decisions, long long* episodes,
                                double* elapsed);
 
+/* The same loop with 2-ply scoring when ply == 2 (two_ply.py:44-150 exact
+ * mode + the worker hook 153-193: the top 4 by V scored alpha*V - beta*W,
+ * alpha 1.0, beta 0.9, softmax(score/T) over the four; 1-ply below 4 moves). */
+long long bgref_selfplay_bench_ply(const float* W1, const float* b1, const float* w2,
+                                   const float* b2, float temperature, uint64_t seed,
+                                   int n_threads, double seconds, int ply,
+                                   long long* decisions, long long* episodes,
+                                   double* elapsed);
+
 #ifdef __cplusplus
 }
 #endif

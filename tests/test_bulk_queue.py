@@ -92,10 +92,10 @@ def test_ring_many_producers_one_consumer():
 def _harvest_like(seed, n_eps):
     rng = np.random.default_rng(seed)
     lens = rng.integers(1, 120, n_eps)
-    hdr = np.zeros((n_eps, 8), np.uint32)
+    hdr = np.zeros((n_eps, 16), np.uint32)
     hdr[:, 0] = rng.integers(0, 4096, n_eps)
     hdr[:, 3] = lens
-    rec = rng.integers(0, 2**32, (int(lens.sum()), 24), dtype=np.uint32)
+    rec = rng.integers(0, 2**32, (int(lens.sum()), 12), dtype=np.uint32)
     return hdr, rec
 
 
@@ -142,5 +142,5 @@ def test_message_pack_round_trip():
     h2, r2 = unpack_message(pack_message(h, r))
     np.testing.assert_array_equal(h, h2)
     np.testing.assert_array_equal(r, r2)
-    h0, r0 = unpack_message(pack_message(np.zeros((0, 8), np.uint32), np.zeros((0, 24), np.uint32)))
-    assert h0.shape == (0, 8) and r0.shape == (0, 24)
+    h0, r0 = unpack_message(pack_message(np.zeros((0, 16), np.uint32), np.zeros((0, 12), np.uint32)))
+    assert h0.shape == (0, 16) and r0.shape == (0, 12)

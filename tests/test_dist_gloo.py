@@ -30,9 +30,9 @@ def _worker(rank, world, port, out):
     got = bdist.broadcast_weights(w, src=0)
     base, n = bdist.lane_block(rank, 4096)
     # rank r finished r+1 episodes with 3*(r+1) records, tagged with its lane block
-    hdr = torch.zeros((rank + 1, 8), dtype=torch.int32)
+    hdr = torch.zeros((rank + 1, 16), dtype=torch.int32)
     hdr[:, 0] = base
-    rec = torch.full((3 * (rank + 1), 24), rank + 7, dtype=torch.int32)
+    rec = torch.full((3 * (rank + 1), 12), rank + 7, dtype=torch.int32)
     res = bdist.gather_episodes(Harvest(hdr, rec), dst=0, keep=True)
     # the asynchronous form (bench.py overlaps it with the next steps) returns the same
     pend = bdist.gather_episodes(Harvest(hdr, rec), dst=0, keep=True, async_op=True)

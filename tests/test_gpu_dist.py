@@ -1,0 +1,95 @@
+"""The multi-GPU path with real engines: two ranks (gloo, both on cuda:0 --
+the rehearsal form of bench.py's one-process-per-GPU run) each drive an
+Engine over their lane block and gather their REAL harvests to rank 0
+(bgx.dist.gather_episodes); rank 0 checks them against one Engine over both
+blocks: same episodes, same records (src/main.py:86-91 spreads the games over
+worker processes; here over GPUs, with RCCL in place of gloo on a node)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, L, steps, out):
+    import sys
+    from conftest import PKG, golden
+    sys.path.insert(0, PKG)
+    import torch
+    import torch.distributed as dist
+    from bgx import Engine
+    from bgx import dist as bdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = {k: golden("weights_seed0.npz")[k] for k in ("W1", "b1", "w2", "b2")}
+    w = bdist.broadcast_weights(w, src=0)
+    base, n = bdist.lane_block(rank, L)
+    e = Engine(lanes=n, lane_base=base, seed=17)
+    e.set_weights(w, 1.5, 1)
+    got = []
+    for chunk in (steps // 2, steps - steps // 2):
+        e.step(chunk)
+        h = e.harvest()
+        res = bdist.gather_episodes(h, dst=0, keep=True, async_op=True).wait()
+        if rank == 0:
+            got.append([(hh.cpu().numpy().view(np.uint32), rr.cpu().numpy().view(np.uint32)) for hh, rr in res[2]])
+    e.close()
+    if rank == 0:
+        out.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gathers_real_harvests(weights_seed0):
+    import torch
+    from bgx import Engine
+    from bgx.records import episode_bounds
+    L, steps = 128, 240
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, L, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # one engine over both lane blocks, same harvest cadence
+    e = Engine(lanes=2 * L, seed=17)
+    e.set_weights(weights_seed0, 1.5, 1)
+    want = []
+    for chunk in (steps // 2, steps - steps // 2):
+        e.step(chunk)
+        h = e.harvest()
+        want.append((h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32)))
+    e.close()
+
+    def by_episode(hdr, rec):
+        offs, _ = episode_bounds(hdr)
+        return {(int(r[0]), int(r[1])): (r.copy(), rec[offs[i]:offs[i + 1]]) for i, r in enumerate(hdr)}
+
+    total = 0
+    for parts, (wh, wr) in zip(got, want):
+        merged = {}
+        for r, (hh, rr) in enumerate(parts):
+            assert np.all((hh[:, 0] >= r * L) & (hh[:, 0] < (r + 1) * L))   # each rank's lane block
+            merged.update(by_episode(hh, rr))
+        ref = by_episode(wh, wr)
+        assert merged.keys() == ref.keys() and len(ref) > 20
+        for key in ref:
+            np.testing.assert_array_equal(merged[key][0], ref[key][0], err_msg=str(key))
+            np.testing.assert_array_equal(merged[key][1], ref[key][1], err_msg=str(key))
+        total += len(ref)
+    assert total > 100

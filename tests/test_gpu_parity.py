@@ -32,18 +32,16 @@ def _run_movegen(ops, boards, player, dice, cap):
     return out.cpu().numpy(), cnt.cpu().numpy()
 
 
-# tier-1 kernel (large-launch "0" / 16-wave block "1") x heavy-doubles
-# hand-off to the block-cooperative tier 2 (off "0" / on "1") x the
-# large-launch kernel: balanced pool "1" (default, 10-wave workgroups) / "5"
-# (5-wave workgroups) / strided per-wave "0"
-MG_MODES = [("0", "0", "1"), ("0", "0", "0"), ("0", "0", "5"), ("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")]
+# tier-1 kernel: the balanced pool kernel of large launches ("0") or the
+# 16-wave block kernel of small ones ("1"), x the table-free rules for
+# doubles / non-doubles (default "0") or the hash-table path for every job ("1")
+MG_MODES = [("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")]
 
 
-@pytest.mark.parametrize("few,coop,pool", MG_MODES)
-def test_movegen_golden_cases(bgx_ops, few, coop, pool, monkeypatch):
+@pytest.mark.parametrize("few,table", MG_MODES)
+def test_movegen_golden_cases(bgx_ops, few, table, monkeypatch):
     monkeypatch.setenv("BGX_MG_FEW", few)
-    monkeypatch.setenv("BGX_MG_COOP", coop)
-    monkeypatch.setenv("BGX_MG_POOL", pool)
+    monkeypatch.setenv("BGX_MG_TEST_TABLE", table)
     d = golden("movegen_cases.npz")
     out, cnt = _run_movegen(bgx_ops, d["boards"], d["player"], d["dice"], cap=1024)
     for i in range(len(d["boards"])):
@@ -94,11 +92,9 @@ def _fuzz_positions(seed, n_games):
     return pos
 
 
-@pytest.mark.parametrize("few,coop,pool", [("0", "0", "1"), ("0", "0", "0"), ("1", "1", "1")])
-def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, few, coop, pool, monkeypatch):
+@pytest.mark.parametrize("few", ["0", "1"])
+def test_movegen_fuzz_all_rolls_vs_oracle(bgx_ops, few, monkeypatch):
     monkeypatch.setenv("BGX_MG_FEW", few)
-    monkeypatch.setenv("BGX_MG_COOP", coop)
-    monkeypatch.setenv("BGX_MG_POOL", pool)
     pos = _fuzz_positions(1234, 40)
     rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
     boards = np.stack([p[0] for p in pos for _ in rolls])
@@ -137,11 +133,12 @@ def _random_positions(seed, n):
     return out
 
 
-@pytest.mark.parametrize("rule", ["0", "4"])
-def test_movegen_random_positions_vs_oracle(bgx_ops, rule, monkeypatch):
-    """Random placements, all 36 rolls; non-doubles by the table-free rule
-    (default) and with it disabled (BGX_MG_EXP=4)."""
-    monkeypatch.setenv("BGX_MG_EXP", rule)
+@pytest.mark.parametrize("table", ["0", "1"])
+def test_movegen_random_positions_vs_oracle(bgx_ops, table, monkeypatch):
+    """Random placements, all 36 rolls; doubles and non-doubles by the
+    table-free rules (default) and all through the hash table
+    (BGX_MG_TEST_TABLE=1)."""
+    monkeypatch.setenv("BGX_MG_TEST_TABLE", table)
     pos = _random_positions(99, 1500)
     rolls = [(a, b) for a in range(1, 7) for b in range(1, 7)]
     boards = np.stack([p[0] for p in pos for _ in rolls])
