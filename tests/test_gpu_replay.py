@@ -62,8 +62,9 @@ def test_replay_reference_trajectories(weights_seed0, fused):
     t = golden("env_traj.npz")
     eps = t["episodes"]
     n = len(eps)
-    pad = 64
-    width = int(max(eps[:, 1])) + pad
+    # after its episode a lane keeps playing (new games on 1-2 rolls): two
+    # draws per env step for the rest of the 300 steps, plus the resets
+    width = int(max(eps[:, 1])) + 2 * 300 + 64
     dice = np.tile(np.array([1, 2], np.uint8), (n, width // 2 + 1))[:, :width].copy()
     for i, (d0, dn, _s0, _sn) in enumerate(eps):
         dice[i, :dn] = t["dice"][d0:d0 + dn]
@@ -124,12 +125,12 @@ def test_scripted_dice_need_greedy_and_report_exhaustion(weights_seed0):
 @pytest.mark.parametrize("ply,k_top,fused", [(1, 4, True), (1, 4, False), (2, 4, False)])
 def test_shard_invariance(weights_seed0, ply, k_top, fused):
     """Two engines over lane blocks [0, L) and [L, 2L) == one engine of 2L lanes."""
-    L, steps = (96, 150) if ply == 1 else (32, 40)
+    L, steps = (96, 150) if ply == 1 else (32, 160)
     kw = dict(seed=7, ply=ply, k_top=k_top, fused=fused)
-    whole = _episodes(_engine(weights_seed0, lanes=2 * L, **kw), steps, chunk=50)
+    whole = _episodes(_engine(weights_seed0, lanes=2 * L, **kw), steps, chunk=80)
     parts = {}
     for base in (0, L):
-        parts.update(_episodes(_engine(weights_seed0, lanes=L, lane_base=base, **kw), steps, chunk=50))
+        parts.update(_episodes(_engine(weights_seed0, lanes=L, lane_base=base, **kw), steps, chunk=80))
     assert len(whole) > 10 and whole.keys() == parts.keys()
     for key in whole:
         np.testing.assert_array_equal(whole[key][0][1:], parts[key][0][1:], err_msg=str(key))   # header (not 'first')
@@ -151,14 +152,18 @@ def _two_ply_scores(w, board, mover, d0, d1, k_top):
     return cand, 1.0 * v[cand] - 0.9 * W, v
 
 
-@pytest.mark.parametrize("k_top,lanes,steps", [(4, 48, 40), (0, 16, 8)])
-def test_engine_2ply_greedy_is_oracle_argmax(weights_seed0, k_top, lanes, steps):
+@pytest.mark.parametrize("k_top,lanes,steps,check", [(4, 48, 150, 700), (0, 16, 150, 120)])
+def test_engine_2ply_greedy_is_oracle_argmax(weights_seed0, k_top, lanes, steps, check):
+    """The first `check` decisions of finished greedy games (the oracle's
+    2-ply costs ~8 ms per candidate in C)."""
     e = _engine(weights_seed0, lanes=lanes, seed=3, ply=2, k_top=k_top, greedy=True)
     got = _episodes(e, steps, chunk=steps)
     e.close()
     n = 0
-    for _key, (_hdr, d) in got.items():
+    for _key, (_hdr, d) in sorted(got.items()):
         for k in range(len(d["action"])):
+            if n >= check:
+                break
             a = int(d["action"][k])
             r = _two_ply_scores(weights_seed0, d["before"][k], int(d["mover"][k]), *d["dice"][k], k_top)
             if r[0] is None:   # fewer than 4 moves: 1-ply argmax
@@ -172,15 +177,15 @@ def test_engine_2ply_greedy_is_oracle_argmax(weights_seed0, k_top, lanes, steps)
                 continue
             assert score[list(cand).index(a)] >= score.max() - 2 * V_TOL, (a, score)
             n += 1
-    assert n > (60 if k_top == 0 else 300)
+    assert n >= check
 
 
 def test_engine_2ply_kall_transitions(weights_seed0):
     from test_gpu_engine import _check_transitions, _collect
     e = _engine(weights_seed0, lanes=64, seed=13, ply=2, k_top=0)
-    hdrs, recs = _collect(e, 60, chunk=30)
+    hdrs, recs = _collect(e, 150, chunk=75)
     e.close()
-    assert _check_transitions(weights_seed0, hdrs, recs, 2) > 500
+    assert _check_transitions(weights_seed0, hdrs, recs, 2) > 2000
 
 
 def test_engine_2ply_k4_sampling_distribution(weights_seed0):
