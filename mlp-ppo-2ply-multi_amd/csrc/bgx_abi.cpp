@@ -168,6 +168,7 @@ struct bgx_engine {
     // movegen tiers), BGX_FUSED_PROF (phase clocks, printed at destroy)
     int force_tier = 0;
     bool prof_enabled = false;
+    int fused_wpc = 1;            // BGX_FUSED_WPC: fused 1-ply workgroups per CU (1 or 2)
     uint8_t* dice_tab = nullptr;  // bgx_engine_set_dice
     std::vector<int> ev_kind;
     double ms_mg = 0, ms_mlp = 0;
@@ -533,6 +534,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         if (const char* g = getenv("BGX_GRAPH")) e->use_graph = atoi(g) != 0;
         if (const char* v = getenv("BGX_MG_TEST_TIER")) e->force_tier = atoi(v);
         e->prof_enabled = getenv("BGX_FUSED_PROF") != nullptr;
+    if (const char* v = getenv("BGX_FUSED_WPC")) e->fused_wpc = atoi(v) == 2 ? 2 : 1;
         e->cfg = *cfg;
         // ring slots: a power of two (slot = record counter & (R - 1) stays exact
         // when the 32-bit counter wraps)
@@ -574,7 +576,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         if (!rc && hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
             rc = fail(BGX_E_HIP, "hipHostMalloc failed");
         e->ovf_cap = 1 << 16;
-        e->ws_waves = 256;   // one global-memory fallback slice per tier-2 block
+        e->ws_waves = 512;   // one global-memory fallback slice per tier-2 block / fused workgroup (<= 2 per CU)
         e->ws_slots = 16384;
         ALLOC(e->ovf_list, e->ovf_cap);
         ALLOC(e->ws, (size_t)e->ws_waves * 5 * e->ws_slots);
@@ -835,6 +837,7 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.ws_slots = e->ws_slots;
     f.ws_words_per_block = (size_t)5 * e->ws_slots;
     f.force_tier = e->force_tier;
+    f.wg_per_cu = e->fused_wpc;
     if (e->prof_enabled) {
         if (!e->fprof) {
             if (dalloc(&e->fprof, (size_t)1024 * 16)) return BGX_E_HIP;

@@ -55,21 +55,38 @@ struct FusedTail {
 constexpr int XS = 88;              // V(s), V(candidates 0..XS-2) of each lane kept in LDS (rest: vbuf)
 constexpr int F_LDS = F_TAIL + (int)sizeof(FusedTail) + FL * XS * 4;
 static_assert(F_LDS <= 160 * 1024, "fits the CU's LDS");
+// Two-workgroups-per-CU layout (WPC = 2): no W region (the MLP reads the
+// fragments from global memory, L2-resident), 128 registers per lane
+constexpr int F_TAIL2 = F_SCR;
+constexpr int F_LDS2 = F_TAIL2 + (int)sizeof(FusedTail) + FL * XS * 4;
+static_assert(2 * F_LDS2 <= 160 * 1024, "two workgroups fit the CU's LDS");
 
-template <bool PROF>
-__global__ __launch_bounds__(64 * NW) void fused_step_kernel(FusedArgs f) {
+template <int WPC> constexpr int fused_lds() { return WPC == 1 ? F_LDS : F_LDS2; }
+
+// WPC = workgroups per CU: 1 (W fragments resident in LDS, 256 registers per
+// lane) or 2 (W read from global memory, 128 registers per lane: the two
+// workgroups' phases interleave on the CU)
+template <bool PROF, int WPC>
+__global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(FusedArgs f) {
     constexpr int NT = 64 * NW;          // threads
     constexpr int LPW = FL / NW;         // lanes per wave
+    constexpr int FTAIL = WPC == 1 ? F_TAIL : F_TAIL2;
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     uint8_t* lds = (uint8_t*)smem;
-    FusedTail& T = *(FusedTail*)(lds + F_TAIL);
-    float* xs = (float*)(lds + F_TAIL + sizeof(FusedTail));   // [FL][XS] lane values
+    FusedTail& T = *(FusedTail*)(lds + FTAIL);
+    float* xs = (float*)(lds + FTAIL + sizeof(FusedTail));   // [FL][XS] lane values
     const EngineDev& e = f.e;
     const int t = (int)threadIdx.x, w = t >> 6, l = lane_id();
     for (int i = t; i < 256; i += NT) T.lut[i] = lut_entry((uint32_t)i, f.feat_scale);
     for (int i = t; i < 128; i += NT) T.w2s[i] = f.rowc[i];
-    uint4* wf = (uint4*)(lds + F_W);   // split-fp16 W fragments, loaded once
-    for (int k = t; k < NFRAG; k += NT) wf[k] = f.wfrag[k];
+    const uint4* wf;   // split-fp16 W fragments: loaded once into LDS, or read from global
+    if constexpr (WPC == 1) {
+        uint4* wl = (uint4*)(lds + F_W);
+        for (int k = t; k < NFRAG; k += NT) wl[k] = f.wfrag[k];
+        wf = wl;
+    } else {
+        wf = f.wfrag;
+    }
 
     MovegenArgs a{};
     a.out_mode = OUT_PACKED_SLOT;
@@ -354,20 +371,33 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
-        const void* ks[] = {(const void*)bgx::fused_step_kernel<false>, (const void*)bgx::fused_step_kernel<true>};
-        for (const void* k : ks)
+        const void* k1[] = {(const void*)bgx::fused_step_kernel<false, 1>, (const void*)bgx::fused_step_kernel<true, 1>};
+        const void* k2[] = {(const void*)bgx::fused_step_kernel<false, 2>, (const void*)bgx::fused_step_kernel<true, 2>};
+        for (const void* k : k1)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS) != hipSuccess)
+                return hipErrorInvalidValue;
+        for (const void* k : k2)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS2) != hipSuccess)
                 return hipErrorInvalidValue;
     }
     if (args->n_steps <= 0 || args->e.L <= 0) return hipSuccess;
     if (args->cap < 1 || args->cap > 2048) return hipErrorInvalidValue;
-    // persistent: at most one workgroup per CU (LDS) and one tier-3 slice each
+    const int wpc = args->wg_per_cu == 2 ? 2 : 1;
+    // persistent: at most wpc workgroups per CU (LDS, registers) and one tier-3 slice each
     const int groups = (args->e.L + bgx::FL - 1) / bgx::FL;
-    int blocks = groups < n_cu ? groups : n_cu;
+    int blocks = groups < n_cu * wpc ? groups : n_cu * wpc;
     if (blocks > args->ws_blocks) blocks = args->ws_blocks;
-    if (args->prof)
-        hipLaunchKernelGGL(bgx::fused_step_kernel<true>, dim3(blocks), dim3(64 * bgx::NW), bgx::F_LDS, stream, *args);
-    else
-        hipLaunchKernelGGL(bgx::fused_step_kernel<false>, dim3(blocks), dim3(64 * bgx::NW), bgx::F_LDS, stream, *args);
+    const dim3 g(blocks), b(64 * bgx::NW);
+    if (wpc == 2) {
+        if (args->prof)
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 2>), g, b, bgx::F_LDS2, stream, *args);
+        else
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 2>), g, b, bgx::F_LDS2, stream, *args);
+    } else {
+        if (args->prof)
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 1>), g, b, bgx::F_LDS, stream, *args);
+        else
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 1>), g, b, bgx::F_LDS, stream, *args);
+    }
     return hipGetLastError();
 }

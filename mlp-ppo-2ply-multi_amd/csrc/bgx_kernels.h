@@ -143,6 +143,8 @@ struct FusedArgs {
     size_t ws_words_per_block;
     int force_tier;              // test hook (BGX_MG_TEST_TIER)
     unsigned long long* prof;    // development (BGX_FUSED_PROF): [gridDim.x][16] phase clocks, or null
+    int wg_per_cu;               // 1: W fragments resident in LDS (256 registers); 2: two workgroups per CU,
+                                 //   W read from global memory (128 registers)
 };
 
 }  // namespace bgx

@@ -445,25 +445,66 @@ def weighted_opponent_response(board, opponent, net):
     return total
 
 
-def gen_two_ply(net0, netc, positions, rng, t0):
-    pick = rng.choice(np.arange(2, len(positions)), size=60, replace=False)
-    B, O, W0, WC = [], [], [], []
+def spread_reply_board(rng):
+    """An afterstate whose replier (PLAYER2 here, moving 23 -> 0) has many
+    checkers spread over open points: 1-1 / 2-2 / 3-3 then give > 50 replies
+    (two_ply.py:119-121's random.sample threshold)."""
+    b = np.zeros(52, np.uint8)
+    pts = rng.choice(np.arange(6, 24), size=11, replace=False)
+    b[24 + pts] = 1
+    b[24 + pts[:4]] += 1
+    b[24 + 0] = 15 - int(b[24:48].sum())
+    b[0:6] = [0, 2, 0, 3, 2, 0]
+    b[18:24] = [2, 2, 2, 1, 1, 0]
+    return b
+
+
+def gen_two_ply(net0, netc, positions, rng, t0, n_pos=400, n_wide=40):
+    """compute_weighted_opponent_response on n_pos afterstates (the first
+    result of a random roll from random / self-play positions) plus n_wide
+    afterstates whose 1-1 / 2-2 / 3-3 reply sets exceed 50."""
+    pick = rng.choice(np.arange(2, len(positions)), size=min(n_pos, len(positions) - 2), replace=False)
+    B, O = [], []
     for i in pick:
         b, pl = positions[int(i)]
-        # the board after the mover's move: the first result of a random roll
         d0, d1 = int(rng.integers(1, 7)), int(rng.integers(1, 7))
         boards, _, _ = ref_moves(b, pl, d0, d1)
-        after = boards[0] if boards else b
-        ib = to_ib(after)
-        opp = P2 if pl == 0 else P1
-        B.append(after); O.append(int(opp))
-        W0.append(weighted_opponent_response(ib, opp, net0))
-        WC.append(weighted_opponent_response(ib, opp, netc))
+        B.append(boards[0] if boards else b)
+        O.append(1 - pl)
+    wide = 0
+    while wide < n_wide:
+        b = spread_reply_board(rng)
+        if max(len(ref_moves(b, 1, d, d)[0]) for d in (1, 2, 3)) > 50:
+            B.append(b)
+            O.append(1)
+            wide += 1
+    W0 = [weighted_opponent_response(to_ib(b), Player(o), net0) for b, o in zip(B, O)]
+    WC = [weighted_opponent_response(to_ib(b), Player(o), netc) for b, o in zip(B, O)]
     np.savez_compressed(os.path.join(OUT, "two_ply.npz"), boards=np.stack(B),
                         opponent=np.array(O, np.uint8), w_seed0=np.array(W0),
                         w_ckpt=np.array(WC))
-    print(f"[gen] two_ply: {len(B)} positions ({time.time() - t0:.1f}s)", flush=True)
+    print(f"[gen] two_ply: {len(B)} positions, {n_wide} with > 50 replies to a small double "
+          f"({time.time() - t0:.1f}s)", flush=True)
+
+
+def main_two_ply():
+    """Regenerate tests/golden/two_ply.npz only (its own seed)."""
+    rng = np.random.default_rng(20261016)
+    t0 = time.time()
+    positions = [(INITIAL.copy(), 0), (INITIAL.copy(), 1)]
+    positions += selfplay_positions(rng, 40)
+    for mode, cnt in (("general", 120), ("bar", 60), ("bearoff", 60), ("race", 30)):
+        positions += [rand_board(rng, mode) for _ in range(cnt)]
+    torch.manual_seed(0)
+    net0 = policy_network.BackgammonPolicyNetwork()
+    netc = policy_network.BackgammonPolicyNetwork()
+    netc.load_state_dict(torch.load(os.path.join(REF, "src/play/backgammon_256_standard_episode_2100000.pth"),
+                                    map_location="cpu", weights_only=True))
+    gen_two_ply(net0, netc, positions, rng, t0)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--only", "two_ply"]:
+        main_two_ply()
+    else:
+        main()

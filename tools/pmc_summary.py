@@ -35,12 +35,15 @@ def group(name):
 
 
 def main(out):
-    res = {"source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
+    res = {"round": os.path.basename(os.path.normpath(out)),
+           "workload": "bench.py defaults: 8,192 lanes per GPU, seeded xavier weights, T=1.5",
+           "source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
                      "fused 1-ply leg (--kernel-include-regex fused_step, 300 steps per dispatch) and 2-ply K=4 leg "
-                     "(--kernel-include-regex 'movegen|mlp_kernel', 60 steps)",
+                     "(--kernel-include-regex 'movegen|mlp_kernel', 60 steps); SQ busy ratios from "
+                     "tools/sq_counters.sh (sq_<leg>.json)",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts 1/2 of wide "
                          "coalesced reads; narrow movegen reads are uncalibrated, the raw value is kept beside it)"}
-    for leg in ("1ply_fused", "2ply"):
+    for leg in ("1ply_fused", "2ply_k4"):
         f = per_kernel(os.path.join(out, f"pmc_{leg}_FETCH_SIZE"))
         w = per_kernel(os.path.join(out, f"pmc_{leg}_WRITE_SIZE"))
         if not f and not w:
@@ -72,6 +75,21 @@ def main(out):
             if g == "fused":
                 legd[g]["steps_per_launch"] = FUSED_STEPS_PER_DISPATCH
                 legd[g]["hbm_bytes_per_step"] = legd[g]["hbm_bytes_per_launch"] / FUSED_STEPS_PER_DISPATCH
+        # SQ counter ratios of the same leg's kernels (tools/sq_summary.py)
+        sq_leg = {"1ply_fused": "1ply", "2ply_k4": "2ply_k4"}[leg]
+        try:
+            sq = json.load(open(os.path.join(out, f"sq_{sq_leg}.json")))["kernels"]
+            for g in ("movegen", "mlp", "fused"):
+                if g in legd:
+                    ks = [k for k in sq if group(k) == g and "movegen_pool" in k or (group(k) == g and g != "movegen")]
+                    if ks:
+                        k = ks[0]
+                        for r in ("valu_busy", "mfma_busy", "lds_busy", "wait_frac", "issue_stall_frac", "waves_per_cu"):
+                            if r in sq[k]:
+                                legd[g][r] = sq[k][r]
+                        legd[g]["sq_kernel"] = k
+        except (OSError, ValueError, KeyError):
+            pass
         res[leg] = legd
     print(json.dumps(res, indent=1))
 
