@@ -475,11 +475,11 @@ int bgx_engine_destroy(bgx_engine* e) {
         hipSetDevice(e->device);
         hipDeviceSynchronize();
         if (e->fprof) {   // development report (BGX_FUSED_PROF): per workgroup-step averages, wall clock 100 MHz
-            std::vector<unsigned long long> p((size_t)1024 * 16);
+            std::vector<unsigned long long> p((size_t)1024 * 32);
             if (hipMemcpy(p.data(), e->fprof, p.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-                double s[16] = {0};
+                double s[32] = {0};
                 for (int b = 0; b < 1024; ++b)
-                    for (int k = 0; k < 14; ++k) s[k] += (double)p[(size_t)b * 16 + k];
+                    for (int k = 0; k < 18; ++k) s[k] += (double)p[(size_t)b * 32 + k];
                 const double n = s[5] > 0 ? s[5] : 1;
                 fprintf(stderr, "[bgx fused prof] us per workgroup step: step+tier1 %.2f tier2 %.2f wload %.2f mlp %.2f "
                         "pick %.2f | mean wave tier-1 job %.2f (%0.f workgroup steps)\n",
@@ -490,6 +490,8 @@ int bgx_engine_destroy(bgx_engine* e) {
                         s[10] / n / 16 / 100);
                 fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
                         s[11] / (s[12] > 0 ? s[12] : 1) / 100);
+                fprintf(stderr, "[bgx fused prof] tier-1 job: doubles %.2f us (%.0f jobs), non-doubles %.2f us (%.0f jobs)\n",
+                        s[14] / (s[15] > 0 ? s[15] : 1) / 100, s[15], s[16] / (s[17] > 0 ? s[17] : 1) / 100, s[17]);
             }
             hipFree(e->fprof);
         }
@@ -840,8 +842,8 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.wg_per_cu = e->fused_wpc;
     if (e->prof_enabled) {
         if (!e->fprof) {
-            if (dalloc(&e->fprof, (size_t)1024 * 16)) return BGX_E_HIP;
-            HIP_TRY(hipMemset(e->fprof, 0, (size_t)1024 * 16 * 8));
+            if (dalloc(&e->fprof, (size_t)1024 * 32)) return BGX_E_HIP;
+            HIP_TRY(hipMemset(e->fprof, 0, (size_t)1024 * 32 * 8));
         }
         f.prof = e->fprof;
     }

@@ -48,6 +48,7 @@ struct FusedTail {
     uint4 lut[256];                 // feature LUT (bgx_mlp.h lut_entry)
     float w2s[128];                 // value-head weights
     int cnt[FL];                    // lane's full candidate count this step (-1: redo in tier 2)
+    int next[2];                    // tier-1 job counters, alternating by step parity
     int pre[FL + 1];                // MLP row prefix over the lanes
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
     unsigned long long n_rows = 0, n_fb = 0, n_steps = 0;
     // development timers (f.prof): phase sums on thread 0, per-wave sums on lane 0
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tj = 0, tc = 0, tw[4] = {0, 0, 0, 0}, t2c = 0, t3n = 0;
+    unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
     constexpr bool prof = PROF;
     auto tick = [&](int k) {
         if (prof && t == 0) {
@@ -117,6 +119,7 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int nlive = e.L - g * FL < FL ? e.L - g * FL : FL;
         for (int v = t; v < nlive; v += NT) lane_load(e, g * FL + v, T.st[v]);
+        if (t == 0) T.next[0] = T.next[1] = NW;
         n_steps += (unsigned long long)nlive * (unsigned long long)f.n_steps;
         __syncthreads();
         for (int step = 0; step < f.n_steps; ++step) {
@@ -134,14 +137,22 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
                 M.S = S1;
                 M.map[l] = 0u;
                 wave_sync();
-                // doubles (the long jobs) first, dealt out snake-wise: wave w takes
-                // positions w and 2 NW - 1 - w of that order (static, no atomics)
+                // the workgroup's jobs in a queue, doubles (the long jobs) first; each
+                // wave takes the next one from an LDS counter until none is left.
+                // The loop holds no workgroup barrier (the tiers that need one run
+                // after it), its index is wave-uniform (lane 0's atomic, read back
+                // with readfirstlane) and only grows, so every wave leaves it.
                 const bool dbl = l < nlive && T.st[l].d0 == T.st[l].d1;
                 const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(l < nlive && !dbl);
                 const int nd = __popc(dmask);
-                for (int q = 0; q < LPW; ++q) {
-                    const int k = (q & 1) ? (q + 1) * NW - 1 - w : q * NW + w;
-                    if (k >= nlive) continue;
+                int* next = &T.next[step & 1];
+                // wave w starts with job w; the counter (preset to NW) hands out the
+                // rest; at most FL iterations, whatever the counter returns
+                int k = w;
+                for (int it = 0; it < FL && k < nlive; ++it) {
+                    int kn = 0;
+                    if (l == 0) kn = atomicAdd(next, 1);
+                    kn = uniform(kn);
                     const int v = k < nd ? select_bit(dmask, k) : select_bit(omask, k - nd);
                     const LaneState& st = T.st[v];
                     if (l < 8)
@@ -149,14 +160,22 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
                     const JobIn in =
                         make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6], st.p, st.d0, st.d1);
                     uint32_t* fin = nullptr;
+                    const unsigned long long q0 = prof ? wall_clock64() : 0ull;
                     const int nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, 0x7FFFFFFF);
                     if (nf >= 0) emit_records<false>(a, g * FL + v, in, fin, nf, 0);
                     wave_sync();
                     if (l == 0) T.cnt[v] = nf;
+                    if (prof) {
+                        const int kd = in.d0 == in.d1 ? 0 : 2;
+                        tjd[kd] += wall_clock64() - q0;
+                        tjd[kd + 1] += 1;
+                    }
+                    k = kn;
                 }
                 if (prof) tj += wall_clock64() - j0;
             }
             __syncthreads();
+            if (t == 0) T.next[(step + 1) & 1] = NW;   // the next step's counter (last used two steps ago)
             tick(0);
             // ---- 1b. jobs that outgrew their slice: the workgroup, one at a time (rare)
             const int cnt_l = l < nlive ? T.cnt[l] : 0;   // lane q < 16 holds lane q's count
@@ -342,7 +361,7 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
         __syncthreads();
     }
     if (prof) {
-        unsigned long long* P = f.prof + (size_t)blockIdx.x * 16;
+        unsigned long long* P = f.prof + (size_t)blockIdx.x * 32;
         if (t == 0) {
             for (int k = 0; k < 6; ++k) atomicAdd(P + k, ph[k]);
             atomicAdd(P + 11, t2c);
@@ -352,6 +371,7 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
         if (l == 0) {
             atomicAdd(P + 6, tj);
             for (int k = 0; k < 4; ++k) atomicAdd(P + 7 + k, tw[k]);
+            for (int k = 0; k < 4; ++k) atomicAdd(P + 14 + k, tjd[k]);
         }
     }
     if (t == 0) {

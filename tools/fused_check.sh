@@ -1,9 +1,13 @@
-# GPU check for the fused 1-ply step kernel: parity tests, then fused vs phased bench legs.
+# fused kernel: correctness (fused == phased, tiers, ragged, greedy, replay) then the phase profile and bench
 set -o pipefail
-export TMPDIR=/tmp; mkdir -p gpurun_out/fused
-timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "fused" > gpurun_out/fused/t.log 2>&1 || { tail -40 gpurun_out/fused/t.log; exit 1; }
-tail -3 gpurun_out/fused/t.log
-for m in "" "--no-fused"; do
-  timeout -k 10 200 python bench.py --steps 400 --warmup 100 --two-ply-steps 0 --kall-steps 0 --no-cpu-baseline --timing-steps 100 $m > gpurun_out/fused/b$m.json 2>gpurun_out/fused/b$m.err || { tail -20 gpurun_out/fused/b$m.err; exit 1; }
-  python -c "import json,sys;d=json.loads(open('gpurun_out/fused/b$m.json').read().strip().splitlines()[-1]);print('$m', round(d['value']/1e6,2),'M', round(d['ms_per_step']*1e3,1),'us/step', json.dumps(d['kernels']))"
-done
+export TMPDIR=/tmp; OUT=gpurun_out/${1:-fcheck}; mkdir -p $OUT
+timeout -k 10 60 python -u -c "
+import sys; sys.path[:0]=['mlp-ppo-2ply-multi_amd','tests']
+import numpy as np
+from conftest import golden
+from bgx import Engine
+w={k: golden('weights_seed0.npz')[k] for k in ('W1','b1','w2','b2')}
+e=Engine(lanes=37, seed=3); e.set_weights(w, 1.5, 1); e.step(5); e.sync(); print('fused smoke ok', e.stats()['env_steps'])
+" 2>&1 | tee $OUT/smoke.log || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_replay.py -k "fused or replay or shard" -v --timeout 120 --timeout-method thread 2>&1 | tee $OUT/tests.log || exit 1
+bash tools/fprof.sh ${1:-fcheck}
