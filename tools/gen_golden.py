@@ -450,10 +450,11 @@ def spread_reply_board(rng):
     checkers spread over open points: 1-1 / 2-2 / 3-3 then give > 50 replies
     (two_ply.py:119-121's random.sample threshold)."""
     b = np.zeros(52, np.uint8)
-    pts = rng.choice(np.arange(6, 24), size=11, replace=False)
+    # points PLAYER1 leaves empty (it holds 1, 3, 4 and 18-22 below): no point is held by both
+    pts = rng.choice(np.array([5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 23]), size=11, replace=False)
     b[24 + pts] = 1
     b[24 + pts[:4]] += 1
-    b[24 + 0] = 15 - int(b[24:48].sum())
+    b[24 + 0] = 15 - int(b[24:48].sum())   # point 0: empty for PLAYER1
     b[0:6] = [0, 2, 0, 3, 2, 0]
     b[18:24] = [2, 2, 2, 1, 1, 0]
     return b
