@@ -29,6 +29,12 @@ struct Mem {
     uint32_t* map;             // [64] parent start marks for one child chunk (kept zero between uses)
     int S, F;
     int force_table = 0;       // test hook (MovegenArgs::force_table): hash-table path for every job
+    // lists of the table-free modes (doubles by path, non-doubles by rule); they
+    // never touch the table, so a slice may lay them over it (pool kernel):
+    // null = use fa / fb / F
+    uint32_t* pa = nullptr;
+    uint32_t* pb = nullptr;
+    int PF = 0;
 };
 
 // LDS (wavefront scope) or global (agent scope) accessors
@@ -544,7 +550,7 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
 // expand_flat without a table: kfn returns ND_DROP for children that an
 // earlier child already produced (nd_first); the rest are appended in order
 template <bool G, typename KeyFn>
-BGX_DEV bool expand_keep(const Mem& M, const Moves& pm, int c, KeyFn kfn, uint32_t* out, int& n_out) {
+BGX_DEV bool expand_keep(const Mem& M, const Moves& pm, int c, KeyFn kfn, uint32_t* out, int& n_out, int cap) {
     const int l = lane_id();
     const int incl = wave_incl_scan(c);
     const int excl = incl - c;
@@ -559,7 +565,7 @@ BGX_DEV bool expand_keep(const Mem& M, const Moves& pm, int c, KeyFn kfn, uint32
         const uint32_t key = kfn(p, select_bit_fast(src, j));
         const bool sv = r < T && key != ND_DROP;
         const uint64_t bm = ballot(sv);
-        if (n_out + 64 > M.F) return false;
+        if (n_out + 64 > cap) return false;
         if (sv) st32<G>(out + n_out + mask_prefix(bm), key);
         n_out += __popcll(bm);
     }
@@ -579,6 +585,10 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
     int inserted = 0;
     uint32_t* fin = M.fa;   // final record list
     int nfin = 0;
+    // the table-free lists (may overlay the table)
+    uint32_t* const pa = M.pa ? M.pa : M.fa;
+    uint32_t* const pb = M.pa ? M.pb : M.fb;
+    const int PFc = M.pa ? M.PF : M.F;
     const bool dbl = in.d0 == in.d1;
     const int d = in.d0;
 
@@ -630,7 +640,8 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                 const uint32_t key = nd_key((uint32_t)ps1, (uint32_t)pt1, ph1, (uint32_t)s2, (uint32_t)t2, h2);
                 return nd_first(R, occ0, pp, ps1, pt1, s2, t2, H, L) ? key : ND_DROP;
             };
-            if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin)) return -1;
+            fin = pa;
+            if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin, PFc)) return -1;
         } else if (two1 || (nH != 1 && two2)) {
             // 2-move records in (pass, i, j) order (handle_non_doubles 43-68, both passes)
             clear_tab<G>(M);
@@ -671,6 +682,8 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         uint32_t* fa = M.fa;
         uint32_t* fb = M.fb;
         if (doubles_by_path(R) && !M.force_table) {
+            fa = pa;
+            fb = pb;
             if (l == 0) st32<G>(fa, PATH_EMPTY);
             sync<G>();
             int n = 1, level = 0;
@@ -691,7 +704,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                     const int incl = wave_incl_scan(c);
                     const int excl = incl - c;
                     const int Tc = lane63(incl);
-                    if (n_out_check(nn, Tc, M.F)) return -1;
+                    if (n_out_check(nn, Tc, PFc)) return -1;
                     for (int cb = 0; cb < Tc; cb += 64) {
                         const int r = cb + l;
                         const int p = flat_parent<G>(M.map, excl, c, cb);

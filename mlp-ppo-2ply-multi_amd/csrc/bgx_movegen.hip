@@ -42,25 +42,37 @@ namespace bgx {
 // long as its unluckiest wave (67 jobs of very different cost each for the
 // 344 k reply jobs of a 4,096-lane K=4 step); here a wave that drew cheap jobs
 // takes more. The next job's board is loaded while the current job runs.
-// PW = 10 waves per workgroup, two workgroups per CU (measured against four
-// 5-wave workgroups: within run noise)
-constexpr int PW = 10;
-constexpr int PF = Slice<S_T1>::F - 8;                  // frontier entries: PW slices + the counter fit
-constexpr int PSL = S_T1 * 8 + 2 * PF * 4 + 64 * 4;     // slice bytes
-static_assert(PW * PSL + 16 <= 80 * 1024, "two 10-wave workgroups per CU");
+// Slice (4 KB per wave): a 64-word parent map, then a region that is either
+// the table-mode layout (256-slot table + two 224-entry frontiers) or, for the
+// table-free modes (doubles by path, non-doubles by rule: most jobs), two
+// 480-entry lists laid over it. With half the round-1 8 KB slice the pool is
+// bound by registers, not LDS: 16-wave workgroups, two per CU, at <= 64 VGPRs
+// = 8 waves per SIMD, the hardware maximum (amdgpu_waves_per_eu). Measured on
+// the 2-ply K=4 reply launch at 8,192 lanes (profiles/r2/ab_pool): 8 KB slices
+// / 5 waves per SIMD 0.64 ms, 4 KB / 7 waves 0.54 ms, 4 KB / 8 waves 0.475 ms.
+constexpr int PW = 16;                                   // waves per workgroup (two per CU)
+constexpr int P_S = 256;                                 // table slots (table mode)
+constexpr int P_F = 224;                                 // table-mode frontier entries
+constexpr int P_PF = 480;                                // table-free list entries
+constexpr int PSL = 64 * 4 + 2 * P_PF * 4;               // slice bytes (4 KB)
+static_assert(P_S * 8 + 2 * P_F * 4 <= 2 * P_PF * 4, "table layout fits the region");
+static_assert(PW * PSL + 16 <= 80 * 1024, "two workgroups per CU");
 
-__global__ __launch_bounds__(64 * PW) void movegen_pool_kernel(MovegenArgs a) {
+__global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(8))) void movegen_pool_kernel(MovegenArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
     __shared__ int next_job;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
-    unsigned long long* sl = smem + (size_t)w * (PSL / 8);
+    uint32_t* sl = (uint32_t*)(smem + (size_t)w * (PSL / 8));
     Mem M;
-    M.tab = sl;
-    M.S = S_T1;
-    M.F = PF;
-    M.fa = (uint32_t*)(sl + S_T1);
-    M.fb = M.fa + PF;
-    M.map = M.fb + PF;
+    M.map = sl;
+    M.tab = (unsigned long long*)(sl + 64);
+    M.S = P_S;
+    M.F = P_F;
+    M.fa = sl + 64 + 2 * P_S;
+    M.fb = M.fa + P_F;
+    M.pa = sl + 64;
+    M.pb = M.pa + P_PF;
+    M.PF = P_PF;
     M.force_table = a.force_table;
     M.map[l] = 0u;
     const int n_jobs = uniform(job_count(a));
