@@ -168,7 +168,7 @@ struct bgx_engine {
     // movegen tiers), BGX_FUSED_PROF (phase clocks, printed at destroy)
     int force_tier = 0;
     bool prof_enabled = false;
-    int fused_wpc = 1;            // BGX_FUSED_WPC: fused 1-ply workgroups per CU (1 or 2)
+    int fused_fl = 0;             // BGX_FUSED_LANES: fused 1-ply lanes per workgroup (16 / 32; 0 = auto)
     uint8_t* dice_tab = nullptr;  // bgx_engine_set_dice
     std::vector<int> ev_kind;
     double ms_mg = 0, ms_mlp = 0;
@@ -536,7 +536,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         if (const char* g = getenv("BGX_GRAPH")) e->use_graph = atoi(g) != 0;
         if (const char* v = getenv("BGX_MG_TEST_TIER")) e->force_tier = atoi(v);
         e->prof_enabled = getenv("BGX_FUSED_PROF") != nullptr;
-    if (const char* v = getenv("BGX_FUSED_WPC")) e->fused_wpc = atoi(v) == 2 ? 2 : 1;
+        if (const char* v = getenv("BGX_FUSED_LANES")) e->fused_fl = atoi(v);
         e->cfg = *cfg;
         // ring slots: a power of two (slot = record counter & (R - 1) stays exact
         // when the 32-bit counter wraps)
@@ -839,7 +839,7 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.ws_slots = e->ws_slots;
     f.ws_words_per_block = (size_t)5 * e->ws_slots;
     f.force_tier = e->force_tier;
-    f.wg_per_cu = e->fused_wpc;
+    f.lanes_per_wg = e->fused_fl;
     if (e->prof_enabled) {
         if (!e->fprof) {
             if (dalloc(&e->fprof, (size_t)1024 * 32)) return BGX_E_HIP;

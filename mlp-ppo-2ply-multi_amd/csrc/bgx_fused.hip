@@ -1,10 +1,10 @@
 // bgx_fused.hip — the 1-ply self-play step fused into one persistent launch.
 //
-// One workgroup owns 16 game lanes and runs n_steps env steps of each, with no
-// kernel boundary between the steps. NW wavefronts per workgroup (8: two lanes
-// per wave and 256 registers each, the default; 16: one lane per wave):
-//   1. movegen: each wave expands its lanes' (board, player, dice) jobs one
-//      after the other in its own 8 KB LDS slice (tier 1, bgx_movegen.h) and
+// One workgroup owns 16 or 32 game lanes (FL) and runs n_steps env steps of
+// each, with no kernel boundary between the steps. 8 wavefronts per workgroup
+// (256 registers each):
+//   1. movegen: the waves take the workgroup's (board, player, dice) jobs
+//      from an LDS queue (doubles first) and expand each in their own 4 KB LDS slice (tier 1, bgx_movegen.h) and
 //      writes the afterstates to the lane's candidate slots; a job that
 //      outgrows the slice is redone after the barrier (tier 2: 32 KB slice, or
 //      with 16 waves the cooperative doubles; tier 3: the workgroup's global
@@ -31,20 +31,22 @@
 
 namespace bgx {
 
-constexpr int FL = 16;                                   // lanes per workgroup
-constexpr int NW = 8;                                    // waves per workgroup (two lanes each, 256 registers)
+constexpr int NW = 8;                                    // waves per workgroup (256 registers each)
 // LDS: [scratch | W fragments (resident for the launch) | tail | lane values]
-//  scratch = 8 tier-1 slices (256-slot table, 416-entry frontiers) during
-//  movegen, the 32 KB tier-2 slice, then the MLP partials + staged rows
-constexpr int S1 = 256, F1 = 416;
-constexpr int SL1 = S1 * 8 + 2 * F1 * 4 + 64 * 4;        // 5,632 B
-constexpr int F_SCR = NW * SL1;
+//  scratch = 8 tier-1 slices (4 KB, the pool kernel's layout: bgx_movegen.hip)
+//  during movegen, the 32 KB tier-2 slice, then the MLP partials + staged rows
+constexpr int P1_S = 256, P1_F = 224, P1_PF = 480;       // table slots / table-mode frontiers / path lists
+constexpr int SL1 = 64 * 4 + 2 * P1_PF * 4;              // 4,096 B
+static_assert(P1_S * 8 + 2 * P1_F * 4 <= 2 * P1_PF * 4, "table layout fits the region");
+constexpr int F_SCR = NW * SL1 > Slice<S_T2>::bytes ? NW * SL1 : Slice<S_T2>::bytes;
 constexpr int F_W = F_SCR;
 constexpr int F_TAIL = F_W + NFRAG * 16;
-static_assert(Slice<S_T2>::bytes <= F_SCR, "32 KB slice fits the scratch");
 constexpr int FT = F_SCR / (4 * 64 * 4 + 32 * 32);        // MLP tiles per batch: partials + staged rows
 
-struct FusedTail {
+// FL = game lanes per workgroup: 16 (two per wave) or 32 (four per wave: the
+// tier-1 queue then holds 32 jobs, so the long doubles jobs of a step are
+// spread over more short ones; used when every CU still gets a workgroup)
+template <int FL> struct FusedTail {
     uint4 lut[256];                 // feature LUT (bgx_mlp.h lut_entry)
     float w2s[128];                 // value-head weights
     int cnt[FL];                    // lane's full candidate count this step (-1: redo in tier 2)
@@ -53,41 +55,28 @@ struct FusedTail {
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
 };
-constexpr int XS = 88;              // V(s), V(candidates 0..XS-2) of each lane kept in LDS (rest: vbuf)
-constexpr int F_LDS = F_TAIL + (int)sizeof(FusedTail) + FL * XS * 4;
-static_assert(F_LDS <= 160 * 1024, "fits the CU's LDS");
-// Two-workgroups-per-CU layout (WPC = 2): no W region (the MLP reads the
-// fragments from global memory, L2-resident), 128 registers per lane
-constexpr int F_TAIL2 = F_SCR;
-constexpr int F_LDS2 = F_TAIL2 + (int)sizeof(FusedTail) + FL * XS * 4;
-static_assert(2 * F_LDS2 <= 160 * 1024, "two workgroups fit the CU's LDS");
+// V(s), V(candidates 0..XS-2) of each lane kept in LDS (the rest: vbuf)
+template <int FL> constexpr int fused_xs() { return FL == 16 ? 88 : 96; }
+template <int FL> constexpr int fused_lds() { return F_TAIL + (int)sizeof(FusedTail<FL>) + FL * fused_xs<FL>() * 4; }
+static_assert(fused_lds<16>() <= 160 * 1024 && fused_lds<32>() <= 160 * 1024, "fits the CU's LDS");
 
-template <int WPC> constexpr int fused_lds() { return WPC == 1 ? F_LDS : F_LDS2; }
-
-// WPC = workgroups per CU: 1 (W fragments resident in LDS, 256 registers per
-// lane) or 2 (W read from global memory, 128 registers per lane: the two
-// workgroups' phases interleave on the CU)
-template <bool PROF, int WPC>
-__global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(FusedArgs f) {
+template <bool PROF, int FL>
+__global__ __launch_bounds__(64 * NW, 2) void fused_step_kernel(FusedArgs f) {
     constexpr int NT = 64 * NW;          // threads
     constexpr int LPW = FL / NW;         // lanes per wave
-    constexpr int FTAIL = WPC == 1 ? F_TAIL : F_TAIL2;
+    constexpr int XS = fused_xs<FL>();
+    static_assert(LPW == 2 || LPW == 4, "lanes run in half-wave pairs");
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     uint8_t* lds = (uint8_t*)smem;
-    FusedTail& T = *(FusedTail*)(lds + FTAIL);
-    float* xs = (float*)(lds + FTAIL + sizeof(FusedTail));   // [FL][XS] lane values
+    FusedTail<FL>& T = *(FusedTail<FL>*)(lds + F_TAIL);
+    float* xs = (float*)(lds + F_TAIL + sizeof(FusedTail<FL>));   // [FL][XS] lane values
     const EngineDev& e = f.e;
     const int t = (int)threadIdx.x, w = t >> 6, l = lane_id();
     for (int i = t; i < 256; i += NT) T.lut[i] = lut_entry((uint32_t)i, f.feat_scale);
     for (int i = t; i < 128; i += NT) T.w2s[i] = f.rowc[i];
-    const uint4* wf;   // split-fp16 W fragments: loaded once into LDS, or read from global
-    if constexpr (WPC == 1) {
-        uint4* wl = (uint4*)(lds + F_W);
-        for (int k = t; k < NFRAG; k += NT) wl[k] = f.wfrag[k];
-        wf = wl;
-    } else {
-        wf = f.wfrag;
-    }
+    uint4* wl = (uint4*)(lds + F_W);     // split-fp16 W fragments, loaded once
+    for (int k = t; k < NFRAG; k += NT) wl[k] = f.wfrag[k];
+    const uint4* wf = wl;
 
     MovegenArgs a{};
     a.out_mode = OUT_PACKED_SLOT;
@@ -127,14 +116,17 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
             if (prof && t == 0) tc = wall_clock64();
             {
                 const unsigned long long j0 = prof ? wall_clock64() : 0ull;
-                unsigned long long* sl = (unsigned long long*)(lds + (size_t)w * SL1);
+                uint32_t* sl = (uint32_t*)(lds + (size_t)w * SL1);
                 Mem M;
-                M.tab = sl;
-                M.F = F1;
-                M.fa = (uint32_t*)(sl + S1);
-                M.fb = M.fa + F1;
-                M.map = M.fb + F1;
-                M.S = S1;
+                M.map = sl;
+                M.tab = (unsigned long long*)(sl + 64);
+                M.S = P1_S;
+                M.F = P1_F;
+                M.fa = sl + 64 + 2 * P1_S;
+                M.fb = M.fa + P1_F;
+                M.pa = sl + 64;
+                M.pb = M.pa + P1_PF;
+                M.PF = P1_PF;
                 M.map[l] = 0u;
                 wave_sync();
                 // the workgroup's jobs in a queue, doubles (the long jobs) first; each
@@ -228,11 +220,13 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
             tick(1);
             const int nr = T.pre[FL];
             n_rows += (unsigned long long)nr;
-            // row r of the workgroup -> its lane
+            // row r of the workgroup -> its lane: the last v with pre[v] <= r
+            // (binary search; lanes without rows have pre[v] == pre[v + 1])
             auto lane_of = [&](int r) -> int {
                 int v = 0;
 #pragma unroll
-                for (int q = 1; q < FL; ++q) v += T.pre[q] <= r ? 1 : 0;
+                for (int step = FL / 2; step >= 1; step >>= 1)
+                    if (T.pre[v + step] <= r) v += step;
                 return v;
             };
             auto stage = [&](int tb, int nt) {   // rows of tiles tb.. into LDS, all loads in flight together
@@ -307,10 +301,10 @@ __global__ __launch_bounds__(64 * NW, WPC == 1 ? 2 : 4) void fused_step_kernel(F
             tick(3);
             // ---- 5. action choice + env step for the wave's lanes (the chosen
             // afterstate is still staged in LDS when the step fit one MLP batch)
-            // (the wave's two lanes side by side, one per half-wave)
-            static_assert(LPW == 2, "one lane per half-wave");
-            {
-                const int v = w * LPW + (l >> 5);
+            // (two of the wave's lanes side by side, one per half-wave)
+#pragma unroll 1
+            for (int pr = 0; pr < LPW / 2; ++pr) {
+                const int v = w * LPW + 2 * pr + (l >> 5);
                 const bool lead = (l & 31) == 0;
                 if (v < nlive) {
                 const int i = g * FL + v;
@@ -391,33 +385,36 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
-        const void* k1[] = {(const void*)bgx::fused_step_kernel<false, 1>, (const void*)bgx::fused_step_kernel<true, 1>};
-        const void* k2[] = {(const void*)bgx::fused_step_kernel<false, 2>, (const void*)bgx::fused_step_kernel<true, 2>};
-        for (const void* k : k1)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS) != hipSuccess)
+        const void* k16[] = {(const void*)bgx::fused_step_kernel<false, 16>, (const void*)bgx::fused_step_kernel<true, 16>};
+        const void* k32[] = {(const void*)bgx::fused_step_kernel<false, 32>, (const void*)bgx::fused_step_kernel<true, 32>};
+        for (const void* k : k16)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::fused_lds<16>()) != hipSuccess)
                 return hipErrorInvalidValue;
-        for (const void* k : k2)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::F_LDS2) != hipSuccess)
+        for (const void* k : k32)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::fused_lds<32>()) != hipSuccess)
                 return hipErrorInvalidValue;
     }
     if (args->n_steps <= 0 || args->e.L <= 0) return hipSuccess;
     if (args->cap < 1 || args->cap > 2048) return hipErrorInvalidValue;
-    const int wpc = args->wg_per_cu == 2 ? 2 : 1;
-    // persistent: at most wpc workgroups per CU (LDS, registers) and one tier-3 slice each
-    const int groups = (args->e.L + bgx::FL - 1) / bgx::FL;
-    int blocks = groups < n_cu * wpc ? groups : n_cu * wpc;
+    // persistent: one workgroup per CU (LDS, registers) and one tier-3 slice each;
+    // 32 lanes per workgroup when that still gives every CU a workgroup
+    const int L = args->e.L;
+    const int fl = args->lanes_per_wg == 16 || args->lanes_per_wg == 32 ? args->lanes_per_wg
+                   : ((L + 31) / 32 >= n_cu ? 32 : 16);
+    const int groups = (L + fl - 1) / fl;
+    int blocks = groups < n_cu ? groups : n_cu;
     if (blocks > args->ws_blocks) blocks = args->ws_blocks;
     const dim3 g(blocks), b(64 * bgx::NW);
-    if (wpc == 2) {
+    if (fl == 32) {
         if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 2>), g, b, bgx::F_LDS2, stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 32>), g, b, bgx::fused_lds<32>(), stream, *args);
         else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 2>), g, b, bgx::F_LDS2, stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 32>), g, b, bgx::fused_lds<32>(), stream, *args);
     } else {
         if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 1>), g, b, bgx::F_LDS, stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 16>), g, b, bgx::fused_lds<16>(), stream, *args);
         else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 1>), g, b, bgx::F_LDS, stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 16>), g, b, bgx::fused_lds<16>(), stream, *args);
     }
     return hipGetLastError();
 }

@@ -126,7 +126,7 @@ struct EngineDev {
 };
 
 // Fused 1-ply lane step (bgx_fused.hip): one persistent launch runs n_steps
-// env steps of every lane; 16 lanes per workgroup advance together.
+// env steps of every lane; the 16 or 32 lanes of a workgroup advance together.
 struct FusedArgs {
     EngineDev e;
     uint32_t* cand;              // [L][cap][8] packed candidate rows, lane-major
@@ -143,8 +143,8 @@ struct FusedArgs {
     size_t ws_words_per_block;
     int force_tier;              // test hook (BGX_MG_TEST_TIER)
     unsigned long long* prof;    // development (BGX_FUSED_PROF): [gridDim.x][16] phase clocks, or null
-    int wg_per_cu;               // 1: W fragments resident in LDS (256 registers); 2: two workgroups per CU,
-                                 //   W read from global memory (128 registers)
+    int lanes_per_wg;            // 16 or 32 game lanes per workgroup; 0: the launcher picks (32 when
+                                 //   every CU still gets a workgroup)
 };
 
 }  // namespace bgx

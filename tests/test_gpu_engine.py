@@ -341,18 +341,19 @@ def _same_runs(a, b):
             np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")
 
 
-@pytest.mark.parametrize("tier", ["", "2", "3"])
-def test_fused_step_matches_phased_engine(weights_seed0, tier, monkeypatch):
-    """The fused 1-ply kernel (one persistent launch per step() call, 16 lanes
-    per workgroup) and the phased engine (movegen / MLP / select launches per
-    step) produce identical episodes and records for the same seed: same
-    afterstates in the same order, V with the same bits, same samples. With
-    BGX_MG_TEST_TIER=2/3 every fused movegen job is redone by the workgroup
-    tiers (cooperative doubles / 32 KB slice, or the global workspace)."""
+@pytest.mark.parametrize("tier,fl", [("", "16"), ("", "32"), ("2", "16"), ("3", "32")])
+def test_fused_step_matches_phased_engine(weights_seed0, tier, fl, monkeypatch):
+    """The fused 1-ply kernel (one persistent launch per step() call, 16 or 32
+    lanes per workgroup: BGX_FUSED_LANES) and the phased engine (movegen / MLP /
+    select launches per step) produce identical episodes and records for the
+    same seed: same afterstates in the same order, V with the same bits, same
+    samples. With BGX_MG_TEST_TIER=2/3 every fused movegen job is redone by the
+    workgroup tiers (32 KB slice, or the global workspace)."""
     lanes, steps = (300, 160) if not tier else (48, 60)
     ref = _engine(weights_seed0, lanes=lanes, seed=17, ply=1, fused=False)
     a = _by_episode(*_collect(ref, steps, chunk=40))
     ref.close()
+    monkeypatch.setenv("BGX_FUSED_LANES", fl)
     if tier:
         monkeypatch.setenv("BGX_MG_TEST_TIER", tier)
     e = _engine(weights_seed0, lanes=lanes, seed=17, ply=1, fused=True)
@@ -381,10 +382,12 @@ def test_2ply_tier1_kernels_agree(weights_seed0, monkeypatch):
     _same_runs(runs[0], runs[1])
 
 
-def test_fused_greedy_and_ragged_lanes(weights_ckpt):
-    """A lane count that is not a multiple of 16 (the last workgroup is partly
-    empty) and greedy play: fused == phased on the shipped checkpoint."""
+@pytest.mark.parametrize("fl", ["16", "32"])
+def test_fused_greedy_and_ragged_lanes(weights_ckpt, fl, monkeypatch):
+    """A lane count that is not a multiple of 16 / 32 (the last workgroup is
+    partly empty) and greedy play: fused == phased on the shipped checkpoint."""
     runs = []
+    monkeypatch.setenv("BGX_FUSED_LANES", fl)
     for fused in (False, True):
         e = _engine(weights_ckpt, lanes=37, seed=9, ply=1, greedy=True, fused=fused)
         runs.append(_by_episode(*_collect(e, 200, chunk=50)))
