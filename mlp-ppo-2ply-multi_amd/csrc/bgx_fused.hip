@@ -149,12 +149,19 @@ __global__ __launch_bounds__(64 * NW, 2) void fused_step_kernel(FusedArgs f) {
                     const LaneState& st = T.st[v];
                     if (l < 8)
                         T.job[v][l] = l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
+                    STAMP_BEGIN;
                     const JobIn in =
                         make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6], st.p, st.d0, st.d1);
+                    STAMP(in.d0 == in.d1 ? 5 : 0);
                     uint32_t* fin = nullptr;
                     const unsigned long long q0 = prof ? wall_clock64() : 0ull;
                     const int nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, 0x7FFFFFFF);
+                    STAMP(in.d0 == in.d1 ? 12 : 13);
                     if (nf >= 0) emit_records<false>(a, g * FL + v, in, fin, nf, 0);
+                    STAMP(in.d0 == in.d1 ? 10 : 3);
+#ifdef BGX_STAMP
+                    if (nf >= 0 && l == 0) atomicAdd(&bgx_stamp_acc[(blockIdx.x & 255) * 32 + (in.d0 == in.d1 ? 15 : 14)], (unsigned long long)nf);
+#endif
                     wave_sync();
                     if (l == 0) T.cnt[v] = nf;
                     if (prof) {
@@ -377,6 +384,20 @@ __global__ __launch_bounds__(64 * NW, 2) void fused_step_kernel(FusedArgs f) {
 }
 
 }  // namespace bgx
+
+#ifdef BGX_STAMP
+// diagnostic builds: the section sums over all CU slots (then zeroed)
+extern "C" int bgx_diag_stamps(unsigned long long* out32) {
+    static unsigned long long h[256 * 32];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(bgx::bgx_stamp_acc), sizeof(h)) != hipSuccess) return -1;
+    for (int k = 0; k < 32; ++k) {
+        out32[k] = 0;
+        for (int b = 0; b < 256; ++b) out32[k] += h[b * 32 + k];
+    }
+    static unsigned long long z[256 * 32];
+    return hipMemcpyToSymbol(HIP_SYMBOL(bgx::bgx_stamp_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t stream) {
     static int n_cu = 0;

@@ -9,6 +9,25 @@
 
 namespace bgx {
 
+// Diagnostic builds only (-DBGX_STAMP, tools/stamp_build.sh): per-section
+// shader-clock sums of the tier-1 job, lane 0 of each wave, per CU slot.
+#ifdef BGX_STAMP
+static __device__ unsigned long long bgx_stamp_acc[256 * 32];
+#define STAMP_BEGIN unsigned long long stamp_last = __builtin_amdgcn_s_memtime()
+#define STAMP(k)                                                                                        \
+    do {                                                                                                \
+        const unsigned long long stamp_c = __builtin_amdgcn_s_memtime();                                \
+        if (__lane_id() == 0) atomicAdd(&bgx_stamp_acc[(blockIdx.x & 255) * 32 + (k)], stamp_c - stamp_last); \
+        stamp_last = stamp_c;                                                                           \
+    } while (0)
+#define STAMP_COUNT(k) \
+    do { if (__lane_id() == 0) atomicAdd(&bgx_stamp_acc[(blockIdx.x & 255) * 32 + (k)], 1ull); } while (0)
+#else
+#define STAMP_BEGIN
+#define STAMP(k)
+#define STAMP_COUNT(k)
+#endif
+
 constexpr unsigned long long EMPTY64 = ~0ull;
 constexpr uint32_t KEY_EMPTY4 = 0xFFFFFu;   // four empty 5-bit fields
 constexpr uint32_t KEYMASK = 0xFFFFFu;
@@ -309,63 +328,60 @@ BGX_DEV JobIn make_job(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint3
 
 // A job's input as loaded (fetch_raw), before the root analysis (decode_job):
 // the split lets a kernel load the next job's words while the current one runs.
+// One register per lane: lane k < 8 holds word k of the packed board (lane
+// k < 13: word k of the u8[52] board in IN_U8 mode), lane 13 the mover and dice
+// (player | d0 << 8 | d1 << 16; not IN_TWOPLY, where they follow from the row
+// and the job index); decode_job reads them back with readlane (SGPRs).
 // IN_TWOPLY rows whose word 7 is SKIP_ROW are skipped (a lane with fewer than
 // four candidates, two_ply.py:67-70 via the engine's top-k).
 constexpr uint32_t SKIP_ROW = 0xFFFFFFFFu;
-struct RawJob { uint4 x, y; int player, d0, d1; };
+struct RawJob { uint32_t v; };
 
 BGX_DEV RawJob fetch_raw(const MovegenArgs& a, int j) {
-    RawJob r;
-    r.player = 0;
-    r.d0 = r.d1 = 0;
+    const int l = lane_id();
+    uint32_t v = 0u;
     if (a.in_mode == IN_U8) {
-        const uint32_t* b = (const uint32_t*)(a.in_u8 + (size_t)j * 52);
-        r.x = make_uint4(pack4(b[0]) | (pack4(b[1]) << 16), pack4(b[2]) | (pack4(b[3]) << 16),
-                         pack4(b[4]) | (pack4(b[5]) << 16), pack4(b[6]) | (pack4(b[7]) << 16));
-        const uint32_t t = b[12];
-        r.y = make_uint4(pack4(b[8]) | (pack4(b[9]) << 16), pack4(b[10]) | (pack4(b[11]) << 16),
-                         (t & 15u) | (((t >> 8) & 15u) << 4) | (((t >> 16) & 15u) << 8) | (((t >> 24) & 15u) << 12),
-                         0u);
-        r.player = a.in_player[j];
-        r.d0 = a.in_dice[2 * j];
-        r.d1 = a.in_dice[2 * j + 1];
-        return r;
-    }
-    int src = j;
-    if (a.in_mode == IN_TWOPLY) {
-        const int row = j / 21;
-        src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
-    }
-    if (src < 0) {
-        r.x = make_uint4(0, 0, 0, 0);
-        r.y = make_uint4(0, 0, 0, SKIP_ROW);
+        if (l < 13) v = ((const uint32_t*)(a.in_u8 + (size_t)j * 52))[l];
     } else {
-        const uint4* p = (const uint4*)(a.in_packed + (size_t)src * 8);
-        r.x = p[0];
-        r.y = p[1];
+        int src = j;
+        if (a.in_mode == IN_TWOPLY) {
+            const int row = j / 21;
+            src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
+        }
+        if (l < 8) v = src < 0 ? (l == 7 ? SKIP_ROW : 0u) : a.in_packed[(size_t)src * 8 + l];
     }
-    if (a.in_mode != IN_TWOPLY) {
-        r.player = a.in_player[j];
-        r.d0 = a.in_dice[2 * j];
-        r.d1 = a.in_dice[2 * j + 1];
-    }
-    return r;
+    if (l == 13 && a.in_mode != IN_TWOPLY)
+        v = (uint32_t)a.in_player[j] | ((uint32_t)a.in_dice[2 * j] << 8) | ((uint32_t)a.in_dice[2 * j + 1] << 16);
+    return {v};
 }
 
+BGX_DEV uint32_t lane_word(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+
 BGX_DEV JobIn decode_job(const MovegenArgs& a, int j, const RawJob& r) {
-    int player = r.player, d0 = r.d0, d1 = r.d1;
+    uint32_t w[7];
+    if (a.in_mode == IN_U8) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) w[k] = pack4(lane_word(r.v, 2 * k)) | (pack4(lane_word(r.v, 2 * k + 1)) << 16);
+        const uint32_t t = lane_word(r.v, 12);
+        w[6] = (t & 15u) | (((t >> 8) & 15u) << 4) | (((t >> 16) & 15u) << 8) | (((t >> 24) & 15u) << 12);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) w[k] = lane_word(r.v, k);
+    }
+    const uint32_t pd = lane_word(r.v, 13);
+    int player = (int)(pd & 255u), d0 = (int)((pd >> 8) & 255u), d1 = (int)(pd >> 16);
     bool skip = false;
     if (a.in_mode == IN_TWOPLY) {
-        skip = r.y.w == SKIP_ROW;
+        skip = lane_word(r.v, 7) == SKIP_ROW;
         // two_ply.py:93-150: the opponent of the candidate's mover replies to every roll
-        player = 1 - (int)((r.y.z >> 16) & 1u);
+        player = 1 - (int)((w[6] >> 16) & 1u);
         int a0 = 1, q = j - 21 * (j / 21);   // DICE_ROLLS order (two_ply.py:10-32)
         while (q >= 7 - a0) { q -= 7 - a0; ++a0; }
         d0 = a0;
         d1 = a0 + q;
     }
-    JobIn in = make_job(r.x.x, r.x.y, r.x.z, r.x.w, r.y.x, r.y.y, r.y.z, player, d0, d1);
-    in.skip = uniform(skip ? 1 : 0) != 0;
+    JobIn in = make_job(w[0], w[1], w[2], w[3], w[4], w[5], w[6], player, d0, d1);
+    in.skip = skip;
     return in;
 }
 
@@ -579,6 +595,7 @@ BGX_DEV bool expand_keep(const Mem& M, const Moves& pm, int c, KeyFn kfn, uint32
 // small-launch kernel then expands the job with the whole block)
 template <bool G>
 BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int heavy_t) {
+    STAMP_BEGIN;
     const Root& R = in.R;
     const int l = lane_id();
     const Node root = root_node(R);
@@ -618,6 +635,8 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
         const bool h1 = v1 && t1 < 24u && ((R.blot >> t1) & 1u);
         if ((two1 || (nH != 1 && two2)) && nd_by_rule(R) && !M.force_table) {
+            STAMP(1);
+            STAMP_COUNT(4);
             // 2-move records without a table (nd_first): a pass-2 parent can
             // only add its chain (s2 = t1) or reverse chain (s2 -> s1) child
             if (pass == 1) {
@@ -642,6 +661,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
             };
             fin = pa;
             if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin, PFc)) return -1;
+            STAMP(2);
         } else if (two1 || (nH != 1 && two2)) {
             // 2-move records in (pass, i, j) order (handle_non_doubles 43-68, both passes)
             clear_tab<G>(M);
@@ -682,6 +702,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         uint32_t* fa = M.fa;
         uint32_t* fb = M.fb;
         if (doubles_by_path(R) && !M.force_table) {
+            STAMP_COUNT(11);
             fa = pa;
             fb = pb;
             if (l == 0) st32<G>(fa, PATH_EMPTY);
@@ -728,6 +749,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                 uint32_t* t = fa; fa = fb; fb = t;
                 n = nn;
                 ++level;
+                if (level <= 2) STAMP(6); else if (level == 3) STAMP(7); else STAMP(8);
             }
             fin = fa;
             if (level == 0) {
@@ -746,6 +768,7 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                     sync<G>();
                 }
             }
+            STAMP(9);
             fin_out = fin;
             return nfin;
         }

@@ -50,6 +50,9 @@ namespace bgx {
 // = 8 waves per SIMD, the hardware maximum (amdgpu_waves_per_eu). Measured on
 // the 2-ply K=4 reply launch at 8,192 lanes (profiles/r2/ab_pool): 8 KB slices
 // / 5 waves per SIMD 0.64 ms, 4 KB / 7 waves 0.54 ms, 4 KB / 8 waves 0.475 ms.
+#ifndef BGX_POOL_WPE
+#define BGX_POOL_WPE 8
+#endif
 constexpr int PW = 16;                                   // waves per workgroup (two per CU)
 constexpr int P_S = 256;                                 // table slots (table mode)
 constexpr int P_F = 224;                                 // table-mode frontier entries
@@ -58,7 +61,7 @@ constexpr int PSL = 64 * 4 + 2 * P_PF * 4;               // slice bytes (4 KB)
 static_assert(P_S * 8 + 2 * P_F * 4 <= 2 * P_PF * 4, "table layout fits the region");
 static_assert(PW * PSL + 16 <= 80 * 1024, "two workgroups per CU");
 
-__global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(8))) void movegen_pool_kernel(MovegenArgs a) {
+__global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_pool_kernel(MovegenArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
     __shared__ int next_job;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
