@@ -626,15 +626,28 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
         mA.n = pass ? mL.n : mH.n;
         int s1 = 0;
         if (v1) s1 = k < mA.nsrc ? select_bit_fast(mA.src, k) : (k == mA.nsrc ? mA.e0 : mA.e1);
-        const Node child = v1 ? apply_move(R, root, s1, dA) : root;
-        Moves m2 = node_moves(R, child, dB, pass ? okH : okL);
+        const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
+        // rule mode (nd_by_rule: nothing on the bar, >= 3 mover checkers outside
+        // home): no node of the two-step tree is on the bar or bearing off, so
+        // the child's move list is its occupancy (the source empties when it
+        // held one checker, t1 fills) with an open destination for dB
+        const bool rule = nd_by_rule(R) && !M.force_table;
+        Moves m2;
+        if (rule) {
+            const uint32_t last1 = nib(R.m0, R.m1, R.m2, s1) == 1u ? 1u << s1 : 0u;
+            m2.src = ((occ24(R.m0, R.m1, R.m2) & ~last1) | (1u << (t1 & 31u))) & (pass ? okH : okL);
+            m2.nsrc = m2.n = __popc(m2.src);
+            m2.e0 = m2.e1 = -1;
+        } else {
+            const Node child = v1 ? apply_move(R, root, s1, dA) : root;
+            m2 = node_moves(R, child, dB, pass ? okH : okL);
+        }
         const int c = v1 ? m2.n : 0;
         const bool two1 = ballot(in32 && pass == 0 && c > 0) != 0ull;
         const bool two2 = ballot(in32 && pass == 1 && c > 0) != 0ull;
         const int nH = mH.n, nL = mL.n;
-        const uint32_t t1 = (uint32_t)dest_of(R, s1, dA);
         const bool h1 = v1 && t1 < 24u && ((R.blot >> t1) & 1u);
-        if ((two1 || (nH != 1 && two2)) && nd_by_rule(R) && !M.force_table) {
+        if ((two1 || (nH != 1 && two2)) && rule) {
             STAMP(1);
             STAMP_COUNT(4);
             // 2-move records without a table (nd_first): a pass-2 parent can
