@@ -248,14 +248,17 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
         const int m = c < 5 ? c : 5;
         float s = 0.0f;
         for (int r = 0; r < 5; ++r) {
-            float v = t[0];
-            int who = gl;
-#pragma unroll
-            for (int off = 8; off >= 1; off >>= 1) {
-                const float ov = __shfl_xor(v, off, 64);
-                const int ow = __shfl_xor(who, off, 64);
-                if (ov > v || (ov == v && ow < who)) { v = ov; who = ow; }
-            }
+            // the group's largest head: a DPP max-scan inside the 16-lane row
+            // (lane 15 of the row ends with the row's max), read back with one
+            // shuffle; the lowest lane holding it pops (ties: lower lane first)
+            float mx = t[0];
+            mx = dpp_maxf<0x111, 0xF>(mx);
+            mx = dpp_maxf<0x112, 0xF>(mx);
+            mx = dpp_maxf<0x114, 0xF>(mx);
+            mx = dpp_maxf<0x118, 0xF>(mx);
+            const float v = __shfl(mx, (lane_id() & 48) | 15, 64);
+            const uint32_t grp = (uint32_t)(ballot(t[0] == v) >> (16 * q)) & 0xFFFFu;
+            const int who = __ffs(grp) - 1;
             if (r < m) s = r ? s + v : v;
             if (who == gl) { t[0] = t[1]; t[1] = t[2]; t[2] = t[3]; t[3] = t[4]; t[4] = -INFINITY; }
         }

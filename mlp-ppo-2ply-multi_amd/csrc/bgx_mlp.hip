@@ -232,11 +232,19 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
                     acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, bq, acc[cur][q], 0, 0, 0);
                     acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, bq, acc[cur][q], 0, 0, 0);
                 }
-                // tile m-1's epilogue, spread over k-steps 0..7 (2 rows per step per board tile)
-                if (m > 0 && s < 8) {
+                // tile m-1's epilogue spread over all 13 k-steps: its 16 row
+                // pairs (p: tile p & 1, rows 2 (p >> 1), +1; each tile's rows in
+                // ascending order) two per step in steps 0..2, one per step after
+                if (m > 0) {
+                    const int p_lo = s < 3 ? 2 * s : s + 3;   // s is unrolled: constants
+                    const int p_n = s < 3 ? 2 : 1;
 #pragma unroll
-                    for (int q = 0; q < NT; ++q) epi_pair(acc[prv][q], m - 1, 2 * s, h, w2s, pm[q]);
-                    if (s == 7) {
+                    for (int k = 0; k < 2; ++k) {
+                        if (k >= p_n) break;
+                        const int p = p_lo + k;
+                        epi_pair(acc[prv][p & 1], m - 1, 2 * (p >> 1), h, w2s, pm[p & 1]);
+                    }
+                    if (s == KSTEPS - 1) {
 #pragma unroll
                         for (int q = 0; q < NT; ++q) {
                             v[q] = m == 1 ? pm[q] : v[q] + pm[q];
