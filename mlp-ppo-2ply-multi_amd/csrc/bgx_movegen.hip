@@ -61,7 +61,15 @@ constexpr int PSL = 64 * 4 + 2 * P_PF * 4;               // slice bytes (4 KB)
 static_assert(P_S * 8 + 2 * P_F * 4 <= 2 * P_PF * 4, "table layout fits the region");
 static_assert(PW * PSL + 16 <= 80 * 1024, "two workgroups per CU");
 
-__global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_pool_kernel(MovegenArgs a) {
+// IN / OUT >= 0: the input / output mode is fixed at compile time (the 2-ply
+// reply launch: IN_TWOPLY, OUT_PACKED_FLAT), so the other modes' code and
+// arguments are dead (fewer live scalar registers); -1: read from the arguments
+template <int IN, int OUT>
+__global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_pool_kernel(
+    MovegenArgs a0) {
+    MovegenArgs a = a0;
+    if constexpr (IN >= 0) a.in_mode = IN;
+    if constexpr (OUT >= 0) a.out_mode = OUT;
     __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
     __shared__ int next_job;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
@@ -275,7 +283,7 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         auto occ = [](int& n, const void* k, int threads, int dflt) {
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n <= 0) n = dflt;
         };
-        occ(per_cup, (const void*)bgx::movegen_pool_kernel, 64 * bgx::PW, 2);
+        occ(per_cup, (const void*)bgx::movegen_pool_kernel<-1, -1>, 64 * bgx::PW, 2);
         occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
         occ(per_cuf, (const void*)bgx::movegen_few_kernel, bgx::NTH, 1);
     }
@@ -306,7 +314,11 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         int blocks = n_cu * per_cup;
         const int need = (a.n_jobs + bgx::PW - 1) / bgx::PW;
         if (!a.n_jobs_dev && need < blocks) blocks = need;
-        hipLaunchKernelGGL(bgx::movegen_pool_kernel, dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
+        if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT)
+            hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>), dim3(blocks),
+                               dim3(64 * bgx::PW), 0, stream, a);
+        else
+            hipLaunchKernelGGL((bgx::movegen_pool_kernel<-1, -1>), dim3(blocks), dim3(64 * bgx::PW), 0, stream, a);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
