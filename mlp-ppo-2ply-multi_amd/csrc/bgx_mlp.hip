@@ -169,8 +169,9 @@ BGX_DEV void epi_pair(const floatx16& acc, int m, int r0, int h, const float* w2
 }
 
 // (Measured and rejected on the 2-ply reply launch, DESIGN.md §4: loading the
-// next tile pair's rows during this pair's MFMAs, and skipping all-zero
-// k-steps -- the branches break the MFMA / epilogue interleave.)
+// next tile pair's rows during this pair's MFMAs, skipping all-zero k-steps --
+// the branches break the MFMA / epilogue interleave -- and a 12-wave variant
+// that rebuilds the feature fragments per m-tile: 903 vs 876 us per launch.)
 __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
     constexpr int NT = 2;
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];

@@ -121,20 +121,29 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
 // the flat output with ONE atomic (a same-address global atomic costs ~11 ns
 // in series: one per job would serialise 4,096 jobs for ~45 us) and each
 // wave writes its records at its prefix within the block.
-__global__ __launch_bounds__(NTH) void movegen_few_kernel(MovegenArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned long long smem[BW * Slice<S_T1>::bytes / 8];
+// Slices as the pool kernel's (4 KB): two blocks per CU; IN / OUT as the pool
+// kernel's (the engine's root launch: IN_PACKED, OUT_PACKED_FLAT).
+template <int IN, int OUT>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(8))) void movegen_few_kernel(MovegenArgs a0) {
+    MovegenArgs a = a0;
+    if constexpr (IN >= 0) a.in_mode = IN;
+    if constexpr (OUT >= 0) a.out_mode = OUT;
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[BW * PSL / 8];
     __shared__ uint32_t wcnt[BW];
     __shared__ int base_s;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
     const int n_jobs = uniform(job_count(a));
-    unsigned long long* sl = smem + (size_t)w * (Slice<S_T1>::bytes / 8);
+    uint32_t* sl = (uint32_t*)(smem + (size_t)w * (PSL / 8));
     Mem M;
-    M.tab = sl;
-    M.F = Slice<S_T1>::F;
-    M.fa = (uint32_t*)(sl + S_T1);
-    M.fb = M.fa + M.F;
-    M.map = M.fb + M.F;
-    M.S = S_T1;
+    M.map = sl;
+    M.tab = (unsigned long long*)(sl + 64);
+    M.S = P_S;
+    M.F = P_F;
+    M.fa = sl + 64 + 2 * P_S;
+    M.fb = M.fa + P_F;
+    M.pa = sl + 64;
+    M.pb = M.pa + P_PF;
+    M.PF = P_PF;
     M.force_table = a.force_table;
     M.map[l] = 0u;
     for (int win = (int)blockIdx.x; win * BW < n_jobs; win += (int)gridDim.x) {
@@ -285,7 +294,7 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         };
         occ(per_cup, (const void*)bgx::movegen_pool_kernel<-1, -1>, 64 * bgx::PW, 2);
         occ(per_cub, (const void*)bgx::movegen_block_kernel, bgx::NTH, 1);
-        occ(per_cuf, (const void*)bgx::movegen_few_kernel, bgx::NTH, 1);
+        occ(per_cuf, (const void*)bgx::movegen_few_kernel<-1, -1>, bgx::NTH, 1);
     }
     // test hooks (parity cross-checks; three getenv per launch, next to a
     // kernel launch's cost): BGX_MG_TEST_TIER=2/3 routes every job to tier 2 / 3;
@@ -309,7 +318,11 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     if (fewm == 1 || (fewm < 0 && few_jobs)) {
         int blocks = a.n_jobs_dev ? n_cu * per_cuf : (a.n_jobs + bgx::BW - 1) / bgx::BW;
         if (blocks > n_cu * per_cuf) blocks = n_cu * per_cuf;
-        hipLaunchKernelGGL(bgx::movegen_few_kernel, dim3(blocks), dim3(bgx::NTH), 0, stream, a);
+        if (a.in_mode == bgx::IN_PACKED && a.out_mode == bgx::OUT_PACKED_FLAT)
+            hipLaunchKernelGGL((bgx::movegen_few_kernel<bgx::IN_PACKED, bgx::OUT_PACKED_FLAT>), dim3(blocks),
+                               dim3(bgx::NTH), 0, stream, a);
+        else
+            hipLaunchKernelGGL((bgx::movegen_few_kernel<-1, -1>), dim3(blocks), dim3(bgx::NTH), 0, stream, a);
     } else {
         int blocks = n_cu * per_cup;
         const int need = (a.n_jobs + bgx::PW - 1) / bgx::PW;
