@@ -31,21 +31,16 @@
 
 namespace bgx {
 
-constexpr int NW = 8;                                    // waves per workgroup (256 registers each)
+// FL = game lanes per workgroup and NW = waves per workgroup: 16 lanes on 8
+// waves (2 per SIMD, 256 registers) when fewer lanes than 32 x CUs, else 32
+// lanes on 12 waves (3 per SIMD, 168 registers): the tier-1 queue then holds
+// 32 jobs, so the long doubles jobs of a step are spread over more short ones,
+// and a third wave per SIMD hides more of each job's latency.
 // LDS: [scratch | W fragments (resident for the launch) | tail | lane values]
-//  scratch = 8 tier-1 slices (4 KB, the pool kernel's layout: bgx_movegen.hip)
-//  during movegen, the 32 KB tier-2 slice, then the MLP partials + staged rows
-constexpr int P1_S = 256, P1_F = 224, P1_PF = 480;       // table slots / table-mode frontiers / path lists
-constexpr int SL1 = 64 * 4 + 2 * P1_PF * 4;              // 4,096 B
-static_assert(P1_S * 8 + 2 * P1_F * 4 <= 2 * P1_PF * 4, "table layout fits the region");
-constexpr int F_SCR = NW * SL1 > Slice<S_T2>::bytes ? NW * SL1 : Slice<S_T2>::bytes;
-constexpr int F_W = F_SCR;
-constexpr int F_TAIL = F_W + NFRAG * 16;
-constexpr int FT = F_SCR / (4 * 64 * 4 + 32 * 32);        // MLP tiles per batch: partials + staged rows
-
-// FL = game lanes per workgroup: 16 (two per wave) or 32 (four per wave: the
-// tier-1 queue then holds 32 jobs, so the long doubles jobs of a step are
-// spread over more short ones; used when every CU still gets a workgroup)
+//  scratch = NW tier-1 slices (the pool kernel's layout, bgx_movegen.hip: a
+//  64-word parent map + a region holding the table-mode or the table-free
+//  lists; 4 KB at 8 waves, 3.5 KB at 12) during movegen, the 32 KB tier-2
+//  slice, then the MLP partials + staged rows
 template <int FL> struct FusedTail {
     uint4 lut[256];                 // feature LUT (bgx_mlp.h lut_entry)
     float w2s[128];                 // value-head weights
@@ -55,17 +50,31 @@ template <int FL> struct FusedTail {
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
 };
-// V(s), V(candidates 0..XS-2) of each lane kept in LDS (the rest: vbuf)
-template <int FL> constexpr int fused_xs() { return FL == 16 ? 88 : 96; }
-template <int FL> constexpr int fused_lds() { return F_TAIL + (int)sizeof(FusedTail<FL>) + FL * fused_xs<FL>() * 4; }
-static_assert(fused_lds<16>() <= 160 * 1024 && fused_lds<32>() <= 160 * 1024, "fits the CU's LDS");
+template <int FL> struct FCfg {
+    static constexpr int NW = FL == 32 ? 12 : 8;
+    static constexpr int WPE = NW / 4;                   // waves per SIMD
+    // (a 128-slot table with 288-entry frontiers at 12 waves: more tier-2 jobs, not faster)
+    static constexpr int P1_S = 256, P1_F = NW > 8 ? 160 : 224, P1_PF = NW > 8 ? 416 : 480;
+    static constexpr int SL1 = 64 * 4 + 2 * P1_PF * 4;
+    static_assert(P1_S * 8 + 2 * P1_F * 4 <= 2 * P1_PF * 4, "table layout fits the region");
+    static constexpr int F_SCR = NW * SL1 > Slice<S_T2>::bytes ? NW * SL1 : Slice<S_T2>::bytes;
+    static constexpr int F_W = F_SCR;
+    static constexpr int F_TAIL = F_W + NFRAG * 16;
+    static constexpr int FT = F_SCR / (4 * 64 * 4 + 32 * 32);   // MLP tiles per batch: partials + staged rows
+    // V(s), V(candidates 0..XS-2) of each lane kept in LDS (the rest: vbuf): as many as fit (<= 96)
+    static constexpr int XS_FIT = (160 * 1024 - F_TAIL - (int)sizeof(FusedTail<FL>)) / (FL * 4);
+    static constexpr int XS = XS_FIT < 96 ? XS_FIT : 96;
+    static constexpr int LDS = F_TAIL + (int)sizeof(FusedTail<FL>) + FL * XS * 4;
+    static_assert(XS >= 24 && LDS <= 160 * 1024, "fits the CU's LDS");
+};
 
 template <bool PROF, int FL>
-__global__ __launch_bounds__(64 * NW, 2) void fused_step_kernel(FusedArgs f) {
+__global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_kernel(FusedArgs f) {
+    using C = FCfg<FL>;
+    constexpr int NW = C::NW, SL1 = C::SL1, F_W = C::F_W, F_TAIL = C::F_TAIL, FT = C::FT, XS = C::XS;
+    constexpr int P1_S = C::P1_S, P1_F = C::P1_F, P1_PF = C::P1_PF;
     constexpr int NT = 64 * NW;          // threads
-    constexpr int LPW = FL / NW;         // lanes per wave
-    constexpr int XS = fused_xs<FL>();
-    static_assert(LPW == 2 || LPW == 4, "lanes run in half-wave pairs");
+    constexpr int PR = (FL + 2 * NW - 1) / (2 * NW);   // rounds of the choice phase (two lanes per wave each)
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     uint8_t* lds = (uint8_t*)smem;
     FusedTail<FL>& T = *(FusedTail<FL>*)(lds + F_TAIL);
@@ -310,8 +319,8 @@ __global__ __launch_bounds__(64 * NW, 2) void fused_step_kernel(FusedArgs f) {
             // afterstate is still staged in LDS when the step fit one MLP batch)
             // (two of the wave's lanes side by side, one per half-wave)
 #pragma unroll 1
-            for (int pr = 0; pr < LPW / 2; ++pr) {
-                const int v = w * LPW + 2 * pr + (l >> 5);
+            for (int pr = 0; pr < PR; ++pr) {
+                const int v = 2 * (pr * NW + w) + (l >> 5);
                 const bool lead = (l & 31) == 0;
                 if (v < nlive) {
                 const int i = g * FL + v;
@@ -409,10 +418,10 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
         const void* k16[] = {(const void*)bgx::fused_step_kernel<false, 16>, (const void*)bgx::fused_step_kernel<true, 16>};
         const void* k32[] = {(const void*)bgx::fused_step_kernel<false, 32>, (const void*)bgx::fused_step_kernel<true, 32>};
         for (const void* k : k16)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::fused_lds<16>()) != hipSuccess)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::FCfg<16>::LDS) != hipSuccess)
                 return hipErrorInvalidValue;
         for (const void* k : k32)
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::fused_lds<32>()) != hipSuccess)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bgx::FCfg<32>::LDS) != hipSuccess)
                 return hipErrorInvalidValue;
     }
     if (args->n_steps <= 0 || args->e.L <= 0) return hipSuccess;
@@ -425,17 +434,17 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
     const int groups = (L + fl - 1) / fl;
     int blocks = groups < n_cu ? groups : n_cu;
     if (blocks > args->ws_blocks) blocks = args->ws_blocks;
-    const dim3 g(blocks), b(64 * bgx::NW);
+    const dim3 g(blocks), b(64 * (fl == 32 ? bgx::FCfg<32>::NW : bgx::FCfg<16>::NW));
     if (fl == 32) {
         if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 32>), g, b, bgx::fused_lds<32>(), stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 32>), g, b, bgx::FCfg<32>::LDS, stream, *args);
         else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 32>), g, b, bgx::fused_lds<32>(), stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 32>), g, b, bgx::FCfg<32>::LDS, stream, *args);
     } else {
         if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 16>), g, b, bgx::fused_lds<16>(), stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 16>), g, b, bgx::FCfg<16>::LDS, stream, *args);
         else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 16>), g, b, bgx::fused_lds<16>(), stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 16>), g, b, bgx::FCfg<16>::LDS, stream, *args);
     }
     return hipGetLastError();
 }
