@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 5
+#define BGX_ABI_VERSION 6
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -187,6 +187,20 @@ int bgx_get_stats(bgx_engine* e, bgx_stats* out);  /* synchronizes */
  * and 0 MLP launches. */
 int bgx_set_timing(bgx_engine* e, int enabled);
 int bgx_get_timing(bgx_engine* e, double* ms_movegen, int* n_movegen, double* ms_mlp, int* n_mlp);
+
+/* TD(0) update on the device: replaces Trainer.update's
+ * per-episode loop (src/agents/trainer.py:81-138: forward, TD(0) target with
+ * gamma * V[t+1] detached, MSE, backward, clip_grad_norm_(clip), Adam step)
+ * with one launch over n_eps episodes of bgx_harvest records (episode e =
+ * records [d_offs[e], d_offs[e+1]), at most 2048 each). d_params / d_adam_m /
+ * d_adam_v: 25,729 fp32 each in state_dict order (fc1.weight [128][198],
+ * fc1.bias, value_head.weight, value_head.bias), updated in place; *d_step =
+ * Adam's step count (incremented per episode); d_metrics[5] (double) +=
+ * per-episode loss, post-clip grad norm, mean |TD error|, mean V, reward sum.
+ * grad_clip <= 0: no clipping. Asynchronous on `stream`. */
+int bgx_td0_update(const uint32_t* d_records, const int32_t* d_offs, int n_eps, float* d_params,
+                   float* d_adam_m, float* d_adam_v, int* d_step, float lr, float gamma, float grad_clip,
+                   double* d_metrics, void* stream);
 
 /* Convert between u8[52] boards and the engine's packed boards (device). */
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream);

@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("BGX_LIB", os.path.join(_HERE, "libbgx.so"))
 c_int, c_float, c_double, c_u64, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                              ctypes.c_uint64, ctypes.c_void_p)
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class BgxError(RuntimeError):
@@ -72,6 +72,8 @@ SIGNATURES = {
     "bgx_set_timing": (c_int, [c_void_p, c_int]),
     "bgx_get_timing": (c_int, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int),
                                ctypes.POINTER(c_double), ctypes.POINTER(c_int)]),
+    "bgx_td0_update": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                               c_float, c_float, c_void_p, c_void_p]),
     "bgx_pack": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "bgx_unpack": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
 }

@@ -10,10 +10,14 @@ configured LR decay is never applied in the reference) (138), then the new
 state_dict goes to the ParameterManager (161).
 
 DeviceTrainer.update_records() runs the same per-episode sequence straight
-from the engine's compact records (the observations are re-encoded on the
-GPU with bgx_encode; no Python Episode objects), and update(episodes) keeps
-the reference's signature. batched=True is a flagged semantic change: one
-Adam step per update on the mean of the per-episode losses.
+from the engine's compact records, and update(episodes) keeps the
+reference's signature. backend="hip" (the default for records) runs the whole
+update as one libbgx launch (bgx_td0_update, csrc/bgx_train.hip: weights in
+registers, Adam moments in place, no host sync per episode); backend="torch"
+runs it as eager torch ops (observations re-encoded with bgx_encode), the
+checker the HIP path is tested against. batched=True (torch only) is a
+flagged semantic change: one Adam step per update on the mean of the
+per-episode losses.
 """
 from __future__ import annotations
 
@@ -33,7 +37,8 @@ MIN_EPISODES_TO_TRAIN = 200   # configuration.py:7
 
 class DeviceTrainer:
     def __init__(self, parameter_manager, device=None, lr=LEARNING_RATE, gamma=GAMMA,
-                 grad_clip=GRAD_CLIP_THRESHOLD, batch_episode_size=MIN_EPISODES_TO_TRAIN, batched=False):
+                 grad_clip=GRAD_CLIP_THRESHOLD, batch_episode_size=MIN_EPISODES_TO_TRAIN, batched=False,
+                 backend="hip"):
         self.parameter_manager = parameter_manager
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.policy_network = BackgammonPolicyNetwork().to(self.device)
@@ -44,7 +49,11 @@ class DeviceTrainer:
         self.grad_clip = grad_clip
         self.batch_episode_size = batch_episode_size
         self.batched = batched
+        if backend not in ("hip", "torch"):
+            raise ValueError(f"backend must be 'hip' or 'torch', not {backend!r}")
+        self.backend = "torch" if batched else backend
         self.total_episodes = 0
+        self._flat = None   # HIP backend state: params / Adam m / v (flat, state_dict order), step
 
     # ------------------------------------------------------------ inputs
     def _from_records(self, headers, records):
@@ -81,9 +90,90 @@ class DeviceTrainer:
     def update_records(self, headers, records):
         """The same update from compact records (headers [n, 16], records [m, 12],
         each episode's records contiguous in header order); any n >= 1."""
+        if self.backend == "hip":
+            return self._update_hip(headers, records)
         return self._update(*self._from_records(headers, records))
 
+    # ------------------------------------------------------------ HIP backend
+    _KEYS = ("fc1.weight", "fc1.bias", "value_head.weight", "value_head.bias")
+
+    def _hip_state(self):
+        """Flat fp32 params / Adam moments (state_dict order) and the step count,
+        taken over from the torch module / optimizer the first time."""
+        if self._flat is None:
+            net, opt = self.policy_network, self.optimizer
+            params = [dict(net.named_parameters())[k] for k in self._KEYS]
+            flat = torch.cat([p.detach().reshape(-1) for p in params]).contiguous()
+            m = torch.zeros_like(flat)
+            v = torch.zeros_like(flat)
+            step = 0
+            st = [opt.state.get(p, {}) for p in params]
+            if all("exp_avg" in x for x in st):
+                m = torch.cat([x["exp_avg"].reshape(-1) for x in st]).contiguous()
+                v = torch.cat([x["exp_avg_sq"].reshape(-1) for x in st]).contiguous()
+                step = int(float(st[0]["step"]))
+            self._flat = {"p": flat, "m": m, "v": v,
+                          "step": torch.tensor([step], dtype=torch.int32, device=self.device)}
+        return self._flat
+
+    def _sync_module(self):
+        """Copy the HIP backend's weights / moments back into the torch module and
+        optimizer (state_dict consumers, and a later torch-backend update)."""
+        f = self._flat
+        net, opt = self.policy_network, self.optimizer
+        params = [dict(net.named_parameters())[k] for k in self._KEYS]
+        o = 0
+        step = int(f["step"].item())
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                p.copy_(f["p"][o:o + n].view_as(p))
+                if step > 0:
+                    st = opt.state[p]
+                    st["exp_avg"] = f["m"][o:o + n].view_as(p).clone()
+                    st["exp_avg_sq"] = f["v"][o:o + n].view_as(p).clone()
+                    st["step"] = torch.tensor(float(step))
+                o += n
+
+    def _update_hip(self, headers, records):
+        from ._lib import check, lib, ptr, stream_handle
+        rec = torch.as_tensor(records).to(self.device)
+        if rec.dtype != torch.int32:
+            rec = rec.view(torch.int32) if rec.dtype == torch.uint32 else rec.to(torch.int32)
+        rec = rec.contiguous()
+        hdr = np.asarray(torch.as_tensor(headers).cpu().numpy()).astype(np.uint32)
+        lens = hdr[:, 3].astype(np.int64)
+        if len(lens) and int(lens.max()) > 2048:
+            raise ValueError("bgx_td0_update: an episode has more than 2048 records")
+        offs = torch.as_tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32), device=self.device)
+        f = self._hip_state()
+        metrics = torch.zeros(5, dtype=torch.float64, device=self.device)
+        n_eps = len(lens)
+        clip = float(self.grad_clip) if self.grad_clip is not None else 0.0
+        check(lib().bgx_td0_update(ptr(rec), ptr(offs), n_eps, ptr(f["p"]), ptr(f["m"]), ptr(f["v"]),
+                                   ptr(f["step"]), float(self.optimizer.param_groups[0]["lr"]),
+                                   float(self.gamma), clip, ptr(metrics), stream_handle(None)),
+              "bgx_td0_update")
+        self.total_episodes += n_eps
+        self._sync_module()
+        a = metrics.tolist()
+        win_counts = {"regular": 0, "gammon": 0, "backgammon": 0}
+        for w in (hdr[:, 5] & 0xFF).tolist():
+            name = WIN_TYPES[int(w)]
+            if name in win_counts:
+                win_counts[name] += 1
+        self.parameter_manager.set_parameters(self.policy_network.state_dict())
+        out = {"loss": a[0], "grad_norm": a[1], "td_error": a[2], "predicted_value": a[3], "reward": a[4],
+               "episode_length": float(lens.sum())}
+        out = {k: v / max(1, n_eps) for k, v in out.items()}
+        out["win_counts"] = win_counts
+        out["episodes"] = n_eps
+        return out
+
     def _update(self, obs, rewards, lens, wins):
+        if self._flat is not None:   # continue from the HIP backend's state
+            self._sync_module()
+            self._flat = None
         net, opt = self.policy_network, self.optimizer
         params = list(net.parameters())
         n_eps = len(lens)

@@ -272,6 +272,30 @@ int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d
     });
 }
 
+int bgx_td0_update(const uint32_t* d_records, const int32_t* d_offs, int n_eps, float* d_params,
+                   float* d_adam_m, float* d_adam_v, int* d_step, float lr, float gamma, float grad_clip,
+                   double* d_metrics, void* stream) {
+    return guarded("bgx_td0_update", [&]() -> int {
+        if (n_eps < 0 || (n_eps > 0 && (!d_records || !d_offs || !d_params || !d_adam_m || !d_adam_v || !d_step ||
+                                        !d_metrics)))
+            return fail(BGX_E_ARG, "bgx_td0_update: bad arguments (n_eps=%d)", n_eps);
+        bgx::TrainArgs a{};
+        a.rec = d_records;
+        a.offs = d_offs;
+        a.n_eps = n_eps;
+        a.params = d_params;
+        a.adam_m = d_adam_m;
+        a.adam_v = d_adam_v;
+        a.step = d_step;
+        a.lr = lr;
+        a.gamma = gamma;
+        a.grad_clip = grad_clip;
+        a.metrics = d_metrics;
+        HIP_TRY(bgx_launch_td0(&a, (hipStream_t)stream));
+        return BGX_OK;
+    });
+}
+
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream) {
     return guarded("bgx_pack", [&]() -> int {
         if (n < 0) return fail(BGX_E_ARG, "bgx_pack: n=%d", n);

@@ -147,6 +147,21 @@ struct FusedArgs {
                                  //   every CU still gets a workgroup)
 };
 
+// TD(0) trainer (bgx_train.hip): one launch over n_eps episodes of compact
+// records (12 words each; the episode e is records [offs[e], offs[e + 1])).
+constexpr int TRAIN_TMAX = 2048;   // longest episode (records) the trainer accepts
+struct TrainArgs {
+    const uint32_t* rec;         // [m][12] experience records (bgx/records.py layout)
+    const int32_t* offs;         // [n_eps + 1]
+    int n_eps;
+    float* params;               // fc1.weight [128][198] | fc1.bias [128] | value_head.weight [128] | value_head.bias
+    float* adam_m;               // Adam first / second moments, same layout
+    float* adam_v;
+    int* step;                   // Adam step count
+    float lr, gamma, grad_clip;  // grad_clip <= 0: no clipping
+    double* metrics;             // [5] += loss, post-clip grad norm, |td| mean, V mean, reward sum (per episode)
+};
+
 }  // namespace bgx
 
 extern "C" {
@@ -167,6 +182,7 @@ hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t
                            const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
                            int sample_k, uint64_t skey, const unsigned long long* salt_dev, hipStream_t stream);
 hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out, hipStream_t stream);
+hipError_t bgx_launch_td0(const bgx::TrainArgs* args, hipStream_t stream);
 hipError_t bgx_launch_harvest(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* out,
                               hipStream_t stream);
 }

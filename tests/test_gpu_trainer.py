@@ -66,8 +66,8 @@ def test_device_trainer_matches_reference_loop(weights_seed0):
     sd0 = BackgammonPolicyNetwork().state_dict()
 
     pm_a, pm_b = _PM(sd0), _PM(sd0)
-    ta = DeviceTrainer(pm_a, device="cuda", batch_episode_size=len(eps))
-    tb = DeviceTrainer(pm_b, device="cuda", batch_episode_size=len(eps))
+    ta = DeviceTrainer(pm_a, device="cuda", batch_episode_size=len(eps), backend="torch")
+    tb = DeviceTrainer(pm_b, device="cuda", batch_episode_size=len(eps), backend="torch")
     ma = ta.update_records(hdr, rec)
     tb.update(eps)
     for k in sd0:   # records path == Episode-object path, bit for bit
@@ -79,3 +79,53 @@ def test_device_trainer_matches_reference_loop(weights_seed0):
     assert ma["episode_length"] == pytest.approx(n_rec / len(eps))
     with pytest.raises(ValueError):
         tb.update(eps[:3])   # trainer.py:49-52: exactly batch_episode_size episodes
+
+
+def test_hip_trainer_matches_torch_and_reference(weights_seed0):
+    """bgx_td0_update (one launch over the episodes, csrc/bgx_train.hip) against
+    the torch backend and the CPU fp32 restatement of trainer.py:81-138: the
+    same weights after 2 x 40 sequential per-episode Adam steps (summation
+    orders differ: tolerance), the same metrics, and the Adam state carried
+    from one update to the next (and into a torch-backend update)."""
+    from bgx import Engine
+    from bgx.episodes import to_episodes
+    from bgx.net import BackgammonPolicyNetwork
+    from bgx.trainer import DeviceTrainer
+    from environments import Episode, Experience, Player
+    eng = Engine(lanes=512, seed=11)
+    eng.set_weights(weights_seed0, 1.5, 1)
+    eng.step(300)
+    h = eng.harvest()
+    eng.close()
+    eps = to_episodes(h, Episode, Experience, Player)[:80]
+    lens = [len(e.experiences) for e in eps]
+    hdr = h.headers[:80].cpu()
+    rec = h.records[:sum(lens)]
+    torch.manual_seed(1)
+    sd0 = BackgammonPolicyNetwork().state_dict()
+    pm_h, pm_t = _PM(sd0), _PM(sd0)
+    th = DeviceTrainer(pm_h, device="cuda", batch_episode_size=40, backend="hip")
+    tt = DeviceTrainer(pm_t, device="cuda", batch_episode_size=40, backend="torch")
+    n0 = sum(lens[:40])
+    mh = th.update_records(hdr[:40], rec[:n0])
+    mt = tt.update_records(hdr[:40], rec[:n0])
+    for k in sd0:
+        torch.testing.assert_close(pm_h.sd[k], pm_t.sd[k], rtol=1e-4, atol=2e-5)
+    for k in ("loss", "grad_norm", "td_error", "predicted_value", "reward", "episode_length"):
+        assert mh[k] == pytest.approx(mt[k], rel=1e-4, abs=1e-6), k
+    assert mh["win_counts"] == mt["win_counts"] and mh["episodes"] == 40
+    # second update: the Adam moments / step continue on the device
+    th.update_records(hdr[40:80], rec[n0:])
+    tt.update_records(hdr[40:80], rec[n0:])
+    for k in sd0:
+        torch.testing.assert_close(pm_h.sd[k], pm_t.sd[k], rtol=2e-4, atol=4e-5)
+    ref = _reference_update(sd0, eps)
+    for k in sd0:   # 80 sequential Adam steps, GPU (one launch per 40) vs CPU fp32
+        torch.testing.assert_close(pm_h.sd[k], ref[k], rtol=2e-4, atol=4e-5)
+    # the module / optimizer state follow the device state: a torch-backend
+    # update continues from it
+    th.backend = "torch"
+    th.update_records(hdr[:40], rec[:n0])
+    tt.update_records(hdr[:40], rec[:n0])
+    for k in sd0:
+        torch.testing.assert_close(pm_h.sd[k], pm_t.sd[k], rtol=3e-4, atol=6e-5)

@@ -44,10 +44,11 @@ def main():
     ap.add_argument("--lanes", type=int, default=4096)
     ap.add_argument("--updates", type=int, default=20)
     ap.add_argument("--batched", action="store_true")
+    ap.add_argument("--backend", default="hip", choices=("hip", "torch"))
     args = ap.parse_args()
     torch.manual_seed(0)
     pm = LocalPM(BackgammonPolicyNetwork().state_dict())
-    trainer = DeviceTrainer(pm, device="cuda", batched=args.batched)
+    trainer = DeviceTrainer(pm, device="cuda", batched=args.batched, backend=args.backend)
     eng = Engine(lanes=args.lanes, seed=0)
     w = dict(zip(("W1", "b1", "w2", "b2"), weights_from(pm.get_parameters())))
     eng.set_weights(w, pm.get_temperature(), pm.version)
@@ -77,7 +78,8 @@ def main():
     print(json.dumps({"updates": done, "episodes_trained": 200 * done, "env_steps": steps * args.lanes,
                       "wall_s": el, "train_s": t_train, "updates_per_s": done / el,
                       "train_episodes_per_s": 200 * done / t_train, "last_loss": m["loss"],
-                      "version": pm.version, "temperature": pm.get_temperature(), "batched": args.batched}))
+                      "version": pm.version, "temperature": pm.get_temperature(), "batched": args.batched,
+                      "backend": trainer.backend}))
 
 
 if __name__ == "__main__":
