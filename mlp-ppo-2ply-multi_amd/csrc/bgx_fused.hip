@@ -6,9 +6,10 @@
 //   1. movegen: the waves take the workgroup's (board, player, dice) jobs
 //      from an LDS queue (doubles first) and expand each in their own 4 KB LDS slice (tier 1, bgx_movegen.h) and
 //      writes the afterstates to the lane's candidate slots; a job that
-//      outgrows the slice is redone after the barrier (tier 2: 32 KB slice, or
-//      with 16 waves the cooperative doubles; tier 3: the workgroup's global
-//      workspace), as movegen_block_kernel does;
+//      outgrows the slice is redone after the barrier (tier 2: a doubles job
+//      outside bear-off by the whole workgroup's path expansion, else a 32 KB
+//      slice in wave 0; tier 3: the workgroup's global workspace), as
+//      movegen_block_kernel does;
 //   2. the LDS that held the slices takes the split-fp16 W fragments, and the
 //      workgroup's rows (the lanes' obs rows + candidates, ~340 per step) are
 //      staged behind them;
@@ -59,6 +60,9 @@ template <int FL> struct FCfg {
     static_assert(P1_S * 8 + 2 * P1_F * 4 <= 2 * P1_PF * 4, "table layout fits the region");
     static constexpr int F_SCR = NW * SL1 > Slice<S_T2>::bytes ? NW * SL1 : Slice<S_T2>::bytes;
     static constexpr int F_W = F_SCR;
+    // tier 2 of a doubles path job: the whole workgroup over the scratch
+    static constexpr int CP_F = 128 * NW;
+    static_assert(sizeof(CoopPathLds<NW, CP_F>) <= F_SCR, "path expansion fits the scratch");
     static constexpr int F_TAIL = F_W + NFRAG * 16;
     static constexpr int FT = F_SCR / (4 * 64 * 4 + 32 * 32);   // MLP tiles per batch: partials + staged rows
     // V(s), V(candidates 0..XS-2) of each lane kept in LDS (the rest: vbuf): as many as fit (<= 96)
@@ -73,6 +77,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     using C = FCfg<FL>;
     constexpr int NW = C::NW, SL1 = C::SL1, F_W = C::F_W, F_TAIL = C::F_TAIL, FT = C::FT, XS = C::XS;
     constexpr int P1_S = C::P1_S, P1_F = C::P1_F, P1_PF = C::P1_PF;
+    constexpr int CP_F = C::CP_F;
     constexpr int NT = 64 * NW;          // threads
     constexpr int PR = (FL + 2 * NW - 1) / (2 * NW);   // rounds of the choice phase (two lanes per wave each)
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -215,7 +220,24 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     if (r < 0 && l == 0) atomicOr(e.err_flags, BGX_ERRF_FALLBACK_OVERFLOW);
                     return r < 0 ? 0 : r;
                 };
-                if (w == 0) {   // tier 2: a 32 KB slice in wave 0, then tier 3
+                // tier 2 of a doubles job outside bear-off / the bar: the path
+                // expansion by every wave over the scratch, then each wave emits
+                // every NW-th chunk of the records
+                int r2 = -1;
+                if (in.d0 == in.d1 && doubles_by_path(in.R) && f.force_tier < 3) {
+                    auto& C = *(CoopPathLds<NW, CP_F>*)lds;
+                    uint32_t* fin = nullptr;
+                    r2 = coop_doubles_path<NW, CP_F>(in, C, fin);
+                    if (r2 >= 0) {
+                        emit_records<false>(a, j, in, fin, r2, 0, 64 * w, 64 * NW);
+                        if (t == 0) {
+                            T.cnt[v] = r2;
+                            a.out_count[j] = r2;
+                        }
+                    }
+                    __syncthreads();
+                }
+                if (r2 < 0 && w == 0) {   // tier 2: a 32 KB slice in wave 0, then tier 3
                     const Mem M2 = lds_mem<S_T2>(smem);
                     int r = f.force_tier >= 3 ? -1 : run_job<false>(a, j, in, M2, fc);
                     if (r < 0) r = run_global();

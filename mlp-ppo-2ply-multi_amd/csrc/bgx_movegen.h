@@ -552,10 +552,18 @@ BGX_DEV bool expand_flat(const Mem& M, const Moves& pm, int c, uint32_t tagbit, 
         bool fresh;
         const uint32_t slot = dedup_insert<G>(M, act, key, ord, fresh);
         inserted += __popcll(ballot(fresh));
-        if (inserted > M.S - (M.S >> 2) || n_out + 64 > M.F) return false;
+        if (inserted > M.S - (M.S >> 2)) {
+            STAMP_COUNT(20);   // (diagnostic builds: overflow cause)
+            return false;
+        }
         sync<G>();
         const bool sv = act && (uint32_t)ld64<G>(M.tab + slot) == ord;
         const uint64_t bm = ballot(sv);
+        // exact: the survivors of this chunk must fit the list
+        if (n_out + __popcll(bm) > M.F) {
+            STAMP_COUNT(21);
+            return false;
+        }
         if (sv) st32<G>(out + n_out + mask_prefix(bm), key | tag);
         n_out += __popcll(bm);
     }
@@ -673,7 +681,10 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                 return nd_first(R, occ0, pp, ps1, pt1, s2, t2, H, L) ? key : ND_DROP;
             };
             fin = pa;
-            if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin, PFc)) return -1;
+            if (!expand_keep<G>(M, m2, cc, kfn, fin, nfin, PFc)) {
+                STAMP_COUNT(22);
+                return -1;
+            }
             STAMP(2);
         } else if (two1 || (nH != 1 && two2)) {
             // 2-move records in (pass, i, j) order (handle_non_doubles 43-68, both passes)
@@ -691,7 +702,10 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                 return nd_key(ps1, pt1, ph1, (uint32_t)s2, t2, h2);
             };
             uint32_t tot;
-            if (!expand_flat<G>(M, m2, cc, 0u, 0u, kfn, fin, nfin, inserted, tot)) return -1;
+            if (!expand_flat<G>(M, m2, cc, 0u, 0u, kfn, fin, nfin, inserted, tot)) {
+                STAMP_COUNT(24);
+                return -1;
+            }
         } else {
             // singles: high-die singles, then (unless pass 2 is skipped) low-die singles
             // (handle_non_doubles 70-81; generate_all_moves.py:40-50)
@@ -738,7 +752,10 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                     const int incl = wave_incl_scan(c);
                     const int excl = incl - c;
                     const int Tc = lane63(incl);
-                    if (n_out_check(nn, Tc, PFc)) return -1;
+                    if (n_out_check(nn, Tc, PFc)) {
+                        STAMP_COUNT(23);
+                        return -1;
+                    }
                     for (int cb = 0; cb < Tc; cb += 64) {
                         const int r = cb + l;
                         const int p = flat_parent<G>(M.map, excl, c, cb);
@@ -803,7 +820,10 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                     return key_insert((uint32_t)__shfl((int)pkey, p, 64), rel_of(s, R.player));
                 };
                 uint32_t tot;
-                if (!expand_flat<G>(M, pm, cnt, pm.n == 1 ? FLAG1 : 0u, T, kfn, fb, nn, inserted, tot)) return -1;
+                if (!expand_flat<G>(M, pm, cnt, pm.n == 1 ? FLAG1 : 0u, T, kfn, fb, nn, inserted, tot)) {
+                    STAMP_COUNT(25);
+                    return -1;
+                }
                 T += tot;
                 if ((int)T > heavy_t) return -2;
             }
@@ -837,9 +857,10 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
 
 // write the job's records (keys in `fin`) as boards at rows base..base+nfin-1
 template <bool G>
-BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const uint32_t* fin, int nfin, int base) {
+BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const uint32_t* fin, int nfin, int base,
+                          int b0 = 0, int bstep = 64) {
     const bool dbl = in.d0 == in.d1;
-    for (int b = 0; b < nfin; b += 64) {
+    for (int b = b0; b < nfin; b += bstep) {
         const int i = b + lane_id();
         if (i < nfin) {
             const uint32_t e = ld32<G>(fin + i);
@@ -891,28 +912,44 @@ struct CoopLds {
     uint32_t wsum[BW];
     uint32_t misc[8];                 // [0] inserted [1] record count [2] emit base [3] heavy mask
 };
-// block-wide exclusive scan of one value per thread; `total` = block sum
-BGX_DEV int block_excl_scan(CoopLds& C, int v, int& total) {
+// block-wide exclusive scan of one value per thread (NWv waves, wsum[NWv] in
+// LDS); `total` = block sum
+template <int NWv>
+BGX_DEV int block_excl_scan_w(uint32_t* wsum, int v, int& total) {
     const int w = (int)threadIdx.x >> 6;
     const int incl = wave_incl_scan(v);
-    if (lane_id() == 63) C.wsum[w] = (uint32_t)incl;
+    if (lane_id() == 63) wsum[w] = (uint32_t)incl;
     __syncthreads();
     int before = 0;
     total = 0;
 #pragma unroll
-    for (int k = 0; k < BW; ++k) {
-        const int t = (int)C.wsum[k];
+    for (int k = 0; k < NWv; ++k) {
+        const int t = (int)wsum[k];
         before += k < w ? t : 0;
         total += t;
     }
     __syncthreads();
     return before + incl - v;
 }
+BGX_DEV int block_excl_scan(CoopLds& C, int v, int& total) { return block_excl_scan_w<BW>(C.wsum, v, total); }
+
+// LDS of the path expansion alone (the fused kernel's tier 2 lays it over
+// its scratch): KF parents / children per level, two parents per thread
+template <int NWv, int KF> struct CoopPathLds {
+    uint32_t fa[KF], fb[KF];
+    uint32_t psrc[KF], ppack[KF], pexcl[KF];
+    uint16_t map[KF];
+    uint32_t wsum[NWv];
+};
 
 // The table-free path expansion (doubles_by_path) by a whole block: per level
 // the parents' filtered move lists and child prefix, then one child per
 // thread written straight to its first-reach slot (no dedup, no ranking).
-BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
+// NWv waves, KF <= 2 * 64 * NWv parents / children per level (-1 beyond).
+template <int NWv, int KF, typename L>
+BGX_DEV int coop_doubles_path(const JobIn& in, L& C, uint32_t*& fin) {
+    static_assert(KF <= 2 * 64 * NWv, "two parents per thread");
+    constexpr int NTH = 64 * NWv;
     const Root& R = in.R;
     const int d = in.d0;
     const int t = (int)threadIdx.x, w = t >> 6;
@@ -941,10 +978,10 @@ BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
             }
         }
         int tot2;
-        const int ex2 = block_excl_scan(C, c[0] | (c[1] << 16), tot2);
+        const int ex2 = block_excl_scan_w<NWv>(C.wsum, c[0] | (c[1] << 16), tot2);
         const int T0 = tot2 & 0xFFFF, T = T0 + (tot2 >> 16);
         if (T == 0) break;                      // uniform
-        if (T > K_F) return -1;
+        if (T > KF) return -1;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
             const int i = hh * NTH + t;
@@ -979,7 +1016,7 @@ BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
     const uint32_t e0 = i0 < n ? fa[i0] : 0u, e1 = i0 + 1 < n ? fa[i0 + 1] : 0u;
     const int f0 = (i0 < n && (e0 & FLAG1)) ? 1 : 0, f1 = (i0 + 1 < n && (e1 & FLAG1)) ? 1 : 0;
     int nf;
-    const int pos = block_excl_scan(C, f0 + f1, nf);
+    const int pos = block_excl_scan_w<NWv>(C.wsum, f0 + f1, nf);
     if (f0) fb[pos] = e0;
     if (f1) fb[pos + f0] = e1;
     __syncthreads();
@@ -989,7 +1026,7 @@ BGX_DEV int coop_doubles_path(const JobIn& in, CoopLds& C, uint32_t*& fin) {
 
 // returns the record count (records in `fin`), -1 = overflow (tier 3)
 BGX_DEV int coop_doubles(const JobIn& in, CoopLds& C, uint32_t*& fin, bool force_table = false) {
-    if (doubles_by_path(in.R) && !force_table) return coop_doubles_path(in, C, fin);
+    if (doubles_by_path(in.R) && !force_table) return coop_doubles_path<BW, K_F>(in, C, fin);
     const Root& R = in.R;
     const int d = in.d0;
     const int t = (int)threadIdx.x, l = lane_id();

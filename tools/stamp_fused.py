@@ -36,7 +36,9 @@ nnd = s[0] / max(1, s[13]) if s[13] else 0
 names = {0: "nd make_job", 1: "nd level-1 (root moves, child moves)", 2: "nd expand_keep", 13: "nd job_records total",
          3: "nd emit", 5: "d make_job", 6: "d levels 0-1", 7: "d level 2", 8: "d level 3", 9: "d records compaction",
          12: "d job_records total", 10: "d emit"}
-res = {"rule nd jobs": s[4], "path d jobs": s[11], "nd results": s[14], "d results": s[15]}
+res = {"rule nd jobs": s[4], "path d jobs": s[11], "nd results": s[14], "d results": s[15],
+       "overflow: table full": s[20], "overflow: table-mode frontier": s[21], "overflow: nd rule list": s[22],
+       "overflow: doubles path list": s[23], "overflow: nd table job": s[24], "overflow: doubles table job": s[25]}
 for k, n in names.items():
     den = s[11] if n.startswith("d ") else s[4]
     res[n] = round(s[k] / max(1, den), 1)
