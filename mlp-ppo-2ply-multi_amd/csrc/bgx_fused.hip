@@ -47,6 +47,7 @@ template <int FL> struct FusedTail {
     float w2s[128];                 // value-head weights
     int cnt[FL];                    // lane's full candidate count this step (-1: redo in tier 2)
     int next[2];                    // tier-1 job counters, alternating by step parity
+    int bdone;                      // last-round lanes stepped so far (this group; see OVL)
     int pre[FL + 1];                // MLP row prefix over the lanes
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
@@ -80,6 +81,12 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     constexpr int CP_F = C::CP_F;
     constexpr int NT = 64 * NW;          // threads
     constexpr int PR = (FL + 2 * NW - 1) / (2 * NW);   // rounds of the choice phase (two lanes per wave each)
+    // OVL: the choice phase's last round is partial (32 lanes on 12 waves: 24 +
+    // 8); it runs without a barrier behind it, so the waves it leaves idle start
+    // the next step's tier-1 jobs of the NA lanes already stepped, and a job of
+    // a last-round lane waits (LDS counter T.bdone) until those lanes are stepped
+    constexpr bool OVL = PR >= 2 && FL < 2 * NW * PR;
+    constexpr int NA = OVL ? 2 * NW * (PR - 1) : FL;
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     uint8_t* lds = (uint8_t*)smem;
     FusedTail<FL>& T = *(FusedTail<FL>*)(lds + F_TAIL);
@@ -122,7 +129,11 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int nlive = e.L - g * FL < FL ? e.L - g * FL : FL;
         for (int v = t; v < nlive; v += NT) lane_load(e, g * FL + v, T.st[v]);
-        if (t == 0) T.next[0] = T.next[1] = NW;
+        if (t == 0) {
+            T.next[0] = T.next[1] = NW;
+            T.bdone = 0;
+        }
+        const int na = nlive < NA ? nlive : NA, nbl = nlive - na;   // lanes stepped before / in the last round
         n_steps += (unsigned long long)nlive * (unsigned long long)f.n_steps;
         __syncthreads();
         for (int step = 0; step < f.n_steps; ++step) {
@@ -148,9 +159,13 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 // The loop holds no workgroup barrier (the tiers that need one run
                 // after it), its index is wave-uniform (lane 0's atomic, read back
                 // with readfirstlane) and only grows, so every wave leaves it.
-                const bool dbl = l < nlive && T.st[l].d0 == T.st[l].d1;
-                const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(l < nlive && !dbl);
+                // (OVL: queue = the NA lanes stepped before the last round, doubles
+                // first, then the last-round lanes, doubles first, read once they are stepped)
+                const bool dbl = l < na && T.st[l].d0 == T.st[l].d1;
+                const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(l < na && !dbl);
                 const int nd = __popc(dmask);
+                uint32_t dmb = 0u, omb = 0u;
+                int ndb = -1;
                 int* next = &T.next[step & 1];
                 // wave w starts with job w; the counter (preset to NW) hands out the
                 // rest; at most FL iterations, whatever the counter returns
@@ -159,7 +174,26 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     int kn = 0;
                     if (l == 0) kn = atomicAdd(next, 1);
                     kn = uniform(kn);
-                    const int v = k < nd ? select_bit(dmask, k) : select_bit(omask, k - nd);
+                    int v;
+                    if (!OVL || k < na) {
+                        v = k < nd ? select_bit(dmask, k) : select_bit(omask, k - nd);
+                    } else {
+                        if (ndb < 0) {
+                            // the last-round lanes of the previous step: every one
+                            // is stepped by a wave that has no barrier ahead of it
+                            const int target = step * nbl;
+                            while (__hip_atomic_load(&T.bdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+                                __builtin_amdgcn_s_sleep(1);
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            const bool inb = l >= na && l < nlive;
+                            const bool db = inb && T.st[l].d0 == T.st[l].d1;
+                            dmb = (uint32_t)ballot(db);
+                            omb = (uint32_t)ballot(inb && !db);
+                            ndb = __popc(dmb);
+                        }
+                        const int kb = k - na;
+                        v = kb < ndb ? select_bit(dmb, kb) : select_bit(omb, kb - ndb);
+                    }
                     const LaneState& st = T.st[v];
                     if (l < 8)
                         T.job[v][l] = l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
@@ -342,6 +376,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             // (two of the wave's lanes side by side, one per half-wave)
 #pragma unroll 1
             for (int pr = 0; pr < PR; ++pr) {
+                const bool last = OVL && pr == PR - 1;
+                if (last) __syncthreads();   // the staged rows are the next step's slices from here on
                 const int v = 2 * (pr * NW + w) + (l >> 5);
                 const bool lead = (l & 31) == 0;
                 if (v < nlive) {
@@ -370,7 +406,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     if (prof) tw[2] += wall_clock64() - s1;
                     uint32_t nb[8];
                     const int r = T.pre[v] + 1 + pick;
-                    if (nr <= FT * 32) {
+                    if (nr <= FT * 32 && !last) {
                         const uint4 bx = rs[2 * r], by = rs[2 * r + 1];
                         nb[0] = bx.x; nb[1] = bx.y; nb[2] = bx.z; nb[3] = bx.w;
                         nb[4] = by.x; nb[5] = by.y; nb[6] = by.z; nb[7] = by.w;
@@ -382,10 +418,14 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 }
                 wave_sync();
                 if (lead) T.st[v] = sr;
+                if (last && lead) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    atomicAdd(&T.bdone, 1);
+                }
                 if (prof) tw[3] += wall_clock64() - s1;
                 }
             }
-            __syncthreads();
+            if (!OVL || step + 1 == f.n_steps) __syncthreads();
             tick(4);
             if (prof && t == 0) ph[5] += 1;
         }
