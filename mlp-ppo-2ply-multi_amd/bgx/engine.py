@@ -55,6 +55,7 @@ class Engine:
             check(lib().bgx_engine_create(self.device.index, ctypes.byref(cfg), ctypes.byref(h)),
                   "bgx_engine_create")
         self._h = h
+        self._empty = None
         self.version = 0
         self.temperature = None
 
@@ -101,6 +102,11 @@ class Engine:
     def harvest(self, stream=None, clone=True) -> Harvest:
         info = HarvestInfo()
         check(lib().bgx_harvest(self._h, ctypes.byref(info), stream_handle(stream)), "bgx_harvest")
+        if info.n_episodes == 0:   # nothing finished: shared empty tensors, no allocation
+            if self._empty is None:
+                self._empty = Harvest(torch.zeros((0, EP_WORDS), dtype=torch.int32, device=self.device),
+                                      torch.zeros((0, REC_WORDS), dtype=torch.int32, device=self.device))
+            return self._empty
         hdr = _wrap(info.d_headers, info.n_episodes * EP_WORDS, self.device).view(-1, EP_WORDS)
         rec = _wrap(info.d_records, info.n_records * REC_WORDS, self.device).view(-1, REC_WORDS)
         if clone:

@@ -159,7 +159,8 @@ struct bgx_engine {
     uint32_t* out_records = nullptr;
     int32_t* d_offs = nullptr;     // [ep_cap + 1]
     uint32_t* d_info = nullptr;    // [4] harvest_scan_kernel totals
-    uint32_t* h_info = nullptr;    // pinned host copy
+    uint32_t* h_info = nullptr;    // host-mapped copy, written by harvest_scan_kernel itself
+    uint32_t* h_info_dev = nullptr;   // its device address
     hipEvent_t hev = nullptr;
     // timing
     bool timing = false;
@@ -599,8 +600,10 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         ALLOC(e->out_records, (size_t)L * ring * bgx::REC_WORDS);
         ALLOC(e->d_offs, (size_t)ep_cap + 1);
         ALLOC(e->d_info, 4);
-        if (!rc && hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
-            rc = fail(BGX_E_HIP, "hipHostMalloc failed");
+        if (!rc && (hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+                        hipSuccess ||
+                    hipHostGetDevicePointer((void**)&e->h_info_dev, e->h_info, 0) != hipSuccess))
+            rc = fail(BGX_E_HIP, "hipHostMalloc (mapped) failed");
         e->ovf_cap = 1 << 16;
         e->ws_waves = 512;   // one global-memory fallback slice per tier-2 block / fused workgroup (<= 2 per CU)
         e->ws_slots = 16384;
@@ -938,11 +941,15 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
             HIP_TRY(hipEventRecord(e->hev, e->last));
             HIP_TRY(hipStreamWaitEvent(s, e->hev, 0));
         }
-        // offsets and totals on the device (harvest_scan_kernel), gather, then ONE
-        // small copy of {episodes, records, error flags} to the host
-        HIP_TRY(bgx_launch_harvest(&e->d, e->d_offs, e->d_info, e->out_records, s));
-        HIP_TRY(hipMemcpyAsync(e->h_info, e->d_info, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        // offsets and totals on the device (harvest_scan_kernel, which also writes
+        // {episodes, records, error flags} straight into host-mapped memory), then
+        // the record gather only when there is an episode to gather
+        HIP_TRY(bgx_launch_harvest_scan(&e->d, e->d_offs, e->d_info, e->h_info_dev, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (e->h_info[0] > 0 && !e->h_info[2]) {
+            HIP_TRY(bgx_launch_harvest_gather(&e->d, e->d_offs, e->d_info, e->out_records, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
         const uint32_t flags = e->h_info[2];
         if (flags) {
             HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));

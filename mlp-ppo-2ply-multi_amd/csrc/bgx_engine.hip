@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void two_ply_reduce_kernel(const float* __rest
 // device so the host needs one small copy: info = {episodes, records, error
 // flags, episodes appended (incl. any past ep_cap)}; the episode list restarts.
 __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t* __restrict__ offs,
-                                                            uint32_t* __restrict__ info) {
+                                                            uint32_t* __restrict__ info, uint32_t* hinfo) {
     __shared__ int wsum[16];
     const unsigned n_raw = *e.ep_count;
     const int n = (int)n_raw < e.ep_cap ? (int)n_raw : e.ep_cap;
@@ -306,10 +306,12 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
     }
     if (t == 0) {
         offs[n] = carry;
-        info[0] = (uint32_t)n;
-        info[1] = (uint32_t)carry;
-        info[2] = *e.err_flags;
-        info[3] = n_raw;
+        const uint32_t v[4] = {(uint32_t)n, (uint32_t)carry, *e.err_flags, n_raw};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            info[k] = v[k];
+            if (hinfo) hinfo[k] = v[k];   // host-mapped (vector stores)
+        }
         *e.ep_count = 0u;
     }
     // every finished episode is harvested now (the list holds them all: ep_cap
@@ -374,11 +376,14 @@ extern "C" hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, dou
                        out);
     return hipGetLastError();
 }
-extern "C" hipError_t bgx_launch_harvest(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info,
-                                         uint32_t* out, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::harvest_scan_kernel, dim3(1), dim3(1024), 0, stream, *e, offsets, info);
-    hipError_t r = hipGetLastError();
-    if (r != hipSuccess) return r;
+extern "C" hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info,
+                                              uint32_t* hinfo, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::harvest_scan_kernel, dim3(1), dim3(1024), 0, stream, *e, offsets, info, hinfo);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
+                                                uint32_t* out, hipStream_t stream) {
     hipLaunchKernelGGL(bgx::gather_kernel, dim3(1024), dim3(256), 0, stream, *e, e->ep_list, offsets, info, out);
     return hipGetLastError();
 }

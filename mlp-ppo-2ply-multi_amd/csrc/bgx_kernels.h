@@ -183,6 +183,10 @@ hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t
                            int sample_k, uint64_t skey, const unsigned long long* salt_dev, hipStream_t stream);
 hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out, hipStream_t stream);
 hipError_t bgx_launch_td0(const bgx::TrainArgs* args, hipStream_t stream);
-hipError_t bgx_launch_harvest(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* out,
-                              hipStream_t stream);
+// harvest: episode offsets / totals (info[4] on the device, hinfo[4] host-mapped
+// or null), then the records gather (launched only when there is an episode)
+hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* hinfo,
+                                   hipStream_t stream);
+hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
+                                     uint32_t* out, hipStream_t stream);
 }
