@@ -375,6 +375,43 @@ BGX_DEV int pick_action(X x, int m, bool greedy, float u) {
 template <typename X>
 BGX_DEV int pick_action_half(X x, int m, bool greedy, float u) {
     const int l = lane_id() & 31, hb = lane_id() & 32;
+    if (m <= 64) {
+        // up to two scores per lane, each read, divided and exponentiated once
+        // (the same terms in the same order as the general loop below)
+        const bool a0 = l < m, a1 = l + 32 < m;
+        const float x0 = a0 ? x(l) : -INFINITY, x1 = a1 ? x(l + 32) : -INFINITY;
+        float mx = fmaxf(fmaxf(-INFINITY, x0), x1);
+        mx = half_last(half_incl_maxf(mx));
+        if (greedy) {
+            float bv = -INFINITY;
+            int bk = 0x7FFFFFFF;
+            if (a0 && x0 > bv) { bv = x0; bk = l; }
+            if (a1 && x1 > bv) { bv = x1; bk = l + 32; }
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) {
+                const float ov = __shfl_xor(bv, off, 64);
+                const int ok = __shfl_xor(bk, off, 64);
+                if (ov > bv || (ov == bv && ok < bk)) { bv = ov; bk = ok; }
+            }
+            return bk;
+        }
+        const float e0 = a0 ? __expf(x0 - mx) : 0.0f, e1 = a1 ? __expf(x1 - mx) : 0.0f;
+        float s = 0.0f;
+        if (a0) s += e0;
+        if (a1) s += e1;
+        const float sum = half_last(half_incl_scanf(s));
+        const float t = u * sum;
+        const float p0 = half_incl_scanf(e0);
+        const uint32_t h0 = (uint32_t)(ballot(a0 && t < 0.0f + p0) >> hb);
+        if (h0) return __ffs(h0) - 1;
+        const float carry = 0.0f + half_last(p0);
+        if (m > 32) {
+            const float p1 = half_incl_scanf(e1);
+            const uint32_t h1 = (uint32_t)(ballot(a1 && t < carry + p1) >> hb);
+            if (h1) return 32 + __ffs(h1) - 1;
+        }
+        return m - 1;
+    }
     float mx = -INFINITY;
     for (int k = l; k < m; k += 32) mx = fmaxf(mx, x(k));
     mx = half_last(half_incl_maxf(mx));

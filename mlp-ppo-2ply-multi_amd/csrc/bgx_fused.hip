@@ -439,6 +439,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             atomicAdd(P + 11, t2c);
             atomicAdd(P + 12, n_fb);
             atomicAdd(P + 13, t3n);
+            atomicAdd(P + 18, (unsigned long long)NW * ph[5]);   // wave-steps
         }
         if (l == 0) {
             atomicAdd(P + 6, tj);
