@@ -511,7 +511,7 @@ int bgx_engine_destroy(bgx_engine* e) {
                         "pick %.2f | mean wave tier-1 job %.2f (%0.f workgroup steps)\n",
                         s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n / 100, s[4] / n / 100,
                         s[6] / nws / 100, n);
-                fprintf(stderr, "[bgx fused prof] mean per wave-step: mlp %.2f | -- %.2f pick %.2f "
+                fprintf(stderr, "[bgx fused prof] mean per wave-step: mlp %.2f | items %.2f pick %.2f "
                         "advance %.2f us\n", s[7] / nws / 100, s[8] / nws / 100, s[9] / nws / 100,
                         s[10] / nws / 100);
                 fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],

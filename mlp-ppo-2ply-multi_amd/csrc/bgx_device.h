@@ -357,8 +357,14 @@ BGX_DEV float half_incl_maxf(float v) {
     v = dpp_maxf<0x142, 0xA>(v);
     return v;
 }
-// the half-wave's lane 31 value (its inclusive total) to every lane of the half
-BGX_DEV float half_last(float v) { return __shfl(v, (lane_id() & 32) + 31, 64); }
+// the half-wave's lane 31 value (its inclusive total) to every lane of the half:
+// two v_readlane (lanes 31 and 63, whatever EXEC is) and a select, no LDS
+// permute round trip (the other half's value, possibly stale, is discarded)
+BGX_DEV float half_last(float v) {
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 31));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+    return (lane_id() & 32) ? b : a;
+}
 BGX_DEV int wave_sum(int v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

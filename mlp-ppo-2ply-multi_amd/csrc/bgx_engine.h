@@ -399,9 +399,10 @@ BGX_DEV int pick_action_half(X x, int m, bool greedy, float u) {
         float s = 0.0f;
         if (a0) s += e0;
         if (a1) s += e1;
-        const float sum = half_last(half_incl_scanf(s));
+        const float ps = half_incl_scanf(s);
+        const float sum = half_last(ps);
         const float t = u * sum;
-        const float p0 = half_incl_scanf(e0);
+        const float p0 = m <= 32 ? ps : half_incl_scanf(e0);   // s == e0 (exactly) when m <= 32
         const uint32_t h0 = (uint32_t)(ballot(a0 && t < 0.0f + p0) >> hb);
         if (h0) return __ffs(h0) - 1;
         const float carry = 0.0f + half_last(p0);

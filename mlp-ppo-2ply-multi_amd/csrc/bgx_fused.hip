@@ -329,6 +329,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 const int nt = n_tiles - tb < FT ? n_tiles - tb : FT;
                 // items: (tile pair, m-tile); an odd last tile runs alone
                 const int npair = (nt + 1) >> 1;
+                const unsigned long long i0 = prof ? wall_clock64() : 0ull;
                 for (int it = w; it < 4 * npair; it += NW) {
                     const int tp = it >> 2, m = it & 3;
                     const int t0 = 2 * tp, c0 = t0 * 32 + (l & 31);
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             mlp_item(wf, T.lut, T.w2s, f.feat_scale, bx0, by0, tile_kmask(bx0, by0), m);
                     }
                 }
+                if (prof) tw[1] += wall_clock64() - i0;   // the wave's MLP items (no barrier)
                 __syncthreads();
                 for (int c = t; c < nt * 32; c += NT) {
                     const int tl = c >> 5, col = c & 31;
