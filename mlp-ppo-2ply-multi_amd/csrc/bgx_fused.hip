@@ -79,6 +79,9 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     constexpr int NW = C::NW, SL1 = C::SL1, F_W = C::F_W, F_TAIL = C::F_TAIL, FT = C::FT, XS = C::XS;
     constexpr int P1_S = C::P1_S, P1_F = C::P1_F, P1_PF = C::P1_PF;
     constexpr int CP_F = C::CP_F;
+    // the cooperative tier 2 at 12 waves only (at 8 waves, 256 registers, its
+    // registers spill in the step loop: 0 -> 19)
+    constexpr bool COOP2 = NW > 8;
     constexpr int NT = 64 * NW;          // threads
     constexpr int PR = (FL + 2 * NW - 1) / (2 * NW);   // rounds of the choice phase (two lanes per wave each)
     // OVL: the choice phase's last round is partial (32 lanes on 12 waves: 24 +
@@ -115,6 +118,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     // development timers (f.prof): phase sums on thread 0, per-wave sums on lane 0
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tj = 0, tc = 0, tw[4] = {0, 0, 0, 0}, t2c = 0, t3n = 0;
     unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
+    unsigned long long twb = 0;                 // tier-1 clocks spent waiting for the last-round lanes
+    unsigned long long tpre = 0;                // tier-1 clocks from a job's queue pop to its expansion
     constexpr bool prof = PROF;
     auto tick = [&](int k) {
         if (prof && t == 0) {
@@ -171,6 +176,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 // rest; at most FL iterations, whatever the counter returns
                 int k = w;
                 for (int it = 0; it < FL && k < nlive; ++it) {
+                    const unsigned long long it0 = prof ? wall_clock64() : 0ull;
                     int kn = 0;
                     if (l == 0) kn = atomicAdd(next, 1);
                     kn = uniform(kn);
@@ -182,9 +188,11 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             // the last-round lanes of the previous step: every one
                             // is stepped by a wave that has no barrier ahead of it
                             const int target = step * nbl;
+                            const unsigned long long b0 = prof ? wall_clock64() : 0ull;
                             while (__hip_atomic_load(&T.bdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
                                 __builtin_amdgcn_s_sleep(1);
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            if (prof) twb += wall_clock64() - b0;
                             const bool inb = l >= na && l < nlive;
                             const bool db = inb && T.st[l].d0 == T.st[l].d1;
                             dmb = (uint32_t)ballot(db);
@@ -203,6 +211,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     STAMP(in.d0 == in.d1 ? 5 : 0);
                     uint32_t* fin = nullptr;
                     const unsigned long long q0 = prof ? wall_clock64() : 0ull;
+                    if (prof) tpre += q0 - it0;
                     const int nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M, fin, 0x7FFFFFFF);
                     STAMP(in.d0 == in.d1 ? 12 : 13);
                     if (nf >= 0) emit_records<false>(a, g * FL + v, in, fin, nf, 0);
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 // expansion by every wave over the scratch, then each wave emits
                 // every NW-th chunk of the records
                 int r2 = -1;
-                if (in.d0 == in.d1 && doubles_by_path(in.R) && f.force_tier < 3) {
+                if (COOP2 && in.d0 == in.d1 && doubles_by_path(in.R) && f.force_tier < 3) {
                     auto& C = *(CoopPathLds<NW, CP_F>*)lds;
                     uint32_t* fin = nullptr;
                     r2 = coop_doubles_path<NW, CP_F>(in, C, fin);
@@ -447,6 +456,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             atomicAdd(P + 6, tj);
             for (int k = 0; k < 4; ++k) atomicAdd(P + 7 + k, tw[k]);
             for (int k = 0; k < 4; ++k) atomicAdd(P + 14 + k, tjd[k]);
+            atomicAdd(P + 19, twb);
+            atomicAdd(P + 20, tpre);
         }
     }
     if (t == 0) {
