@@ -504,7 +504,7 @@ int bgx_engine_destroy(bgx_engine* e) {
             if (hipMemcpy(p.data(), e->fprof, p.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
                 double s[32] = {0};
                 for (int b = 0; b < 1024; ++b)
-                    for (int k = 0; k < 21; ++k) s[k] += (double)p[(size_t)b * 32 + k];
+                    for (int k = 0; k < 23; ++k) s[k] += (double)p[(size_t)b * 32 + k];
                 const double n = s[5] > 0 ? s[5] : 1;
                 const double nws = s[18] > 0 ? s[18] : 1;   // wave-steps
                 fprintf(stderr, "[bgx fused prof] us per workgroup step: step+tier1 %.2f tier2 %.2f wload %.2f mlp %.2f "
@@ -515,7 +515,8 @@ int bgx_engine_destroy(bgx_engine* e) {
                         "advance %.2f us\n", s[7] / nws / 100, s[8] / nws / 100, s[9] / nws / 100,
                         s[10] / nws / 100);
                 fprintf(stderr, "[bgx fused prof] tier-1 wait for the last-round lanes: %.2f us, queue pop to expansion "
-                        "%.2f us per wave-step\n", s[19] / nws / 100, s[20] / nws / 100);
+                        "%.2f us per wave-step (pop + lane %.2f, words + root %.2f)\n", s[19] / nws / 100, s[20] / nws / 100,
+                        s[21] / nws / 100, s[22] / nws / 100);
                 fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
                         s[11] / (s[12] > 0 ? s[12] : 1) / 100);
                 fprintf(stderr, "[bgx fused prof] tier-1 job: doubles %.2f us (%.0f jobs), non-doubles %.2f us (%.0f jobs)\n",

@@ -225,9 +225,20 @@ BGX_DEV Moves node_moves(const Root& r, const Node& n, int d, uint32_t okd) {
 }
 
 // k-th set bit of m (k < popc(m))
+// position of the k-th (0-based) set bit of m, -1 if m has at most k set bits:
+// five narrowing steps (16 / 8 / 4 / 2 / 1 bits), no loop over k
 BGX_DEV int select_bit(uint32_t m, int k) {
-    for (int i = 0; i < k; ++i) m &= m - 1u;
-    return __ffs(m) - 1;
+    int base = 0, c = __popc(m & 0xFFFFu);
+    if (k >= c) { k -= c; m >>= 16; base += 16; }
+    c = __popc(m & 0xFFu);
+    if (k >= c) { k -= c; m >>= 8; base += 8; }
+    c = __popc(m & 0xFu);
+    if (k >= c) { k -= c; m >>= 4; base += 4; }
+    c = __popc(m & 0x3u);
+    if (k >= c) { k -= c; m >>= 2; base += 2; }
+    c = (int)(m & 1u);
+    if (k >= c) { k -= c; m >>= 1; base += 1; }
+    return (k == 0 && (m & 1u)) ? base : -1;
 }
 BGX_DEV int move_source(const Moves& mv, int k) {
     if (k < mv.nsrc) return select_bit(mv.src, k);

@@ -120,6 +120,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
     unsigned long long twb = 0;                 // tier-1 clocks spent waiting for the last-round lanes
     unsigned long long tpre = 0;                // tier-1 clocks from a job's queue pop to its expansion
+    unsigned long long tpa = 0, tpm = 0;        // ... of which: queue pop + lane lookup, job words + root analysis
     constexpr bool prof = PROF;
     auto tick = [&](int k) {
         if (prof && t == 0) {
@@ -202,6 +203,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                         const int kb = k - na;
                         v = kb < ndb ? select_bit(dmb, kb) : select_bit(omb, kb - ndb);
                     }
+                    const unsigned long long ia = prof ? wall_clock64() : 0ull;
+                    if (prof) tpa += ia - it0;
                     const LaneState& st = T.st[v];
                     if (l < 8)
                         T.job[v][l] = l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
@@ -209,6 +212,11 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     const JobIn in =
                         make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6], st.p, st.d0, st.d1);
                     STAMP(in.d0 == in.d1 ? 5 : 0);
+                    if (prof) {
+                        // make the root analysis finish before the clock (its first use)
+                        __builtin_amdgcn_s_waitcnt(0);
+                        tpm += wall_clock64() - ia;
+                    }
                     uint32_t* fin = nullptr;
                     const unsigned long long q0 = prof ? wall_clock64() : 0ull;
                     if (prof) tpre += q0 - it0;
@@ -458,6 +466,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             for (int k = 0; k < 4; ++k) atomicAdd(P + 14 + k, tjd[k]);
             atomicAdd(P + 19, twb);
             atomicAdd(P + 20, tpre);
+            atomicAdd(P + 21, tpa);
+            atomicAdd(P + 22, tpm);
         }
     }
     if (t == 0) {
