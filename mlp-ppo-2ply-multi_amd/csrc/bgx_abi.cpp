@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <exception>
 #include <new>
+#include <algorithm>
 #include <vector>
 
 #include "bgx.h"
@@ -521,6 +522,33 @@ int bgx_engine_destroy(bgx_engine* e) {
                         s[11] / (s[12] > 0 ? s[12] : 1) / 100);
                 fprintf(stderr, "[bgx fused prof] tier-1 job: doubles %.2f us (%.0f jobs), non-doubles %.2f us (%.0f jobs)\n",
                         s[14] / (s[15] > 0 ? s[15] : 1) / 100, s[15], s[16] / (s[17] > 0 ? s[17] : 1) / 100, s[17]);
+                // the last launch, per workgroup: duration spread, dispatch skew, and the
+                // rows / tier-2 jobs of the slowest vs the median workgroup
+                std::vector<std::pair<double, int>> dur;
+                unsigned long long b_min = ~0ull, b_max = 0, e_max = 0;
+                for (int b = 0; b < 1024; ++b) {
+                    const unsigned long long* q = &p[(size_t)b * 32];
+                    if (q[25] <= q[24]) continue;
+                    dur.push_back({(double)(q[25] - q[24]) / 100.0, b});
+                    b_min = q[24] < b_min ? q[24] : b_min;
+                    b_max = q[24] > b_max ? q[24] : b_max;
+                    e_max = q[25] > e_max ? q[25] : e_max;
+                }
+                if (!dur.empty()) {
+                    std::sort(dur.begin(), dur.end());
+                    double mean = 0;
+                    for (auto& d : dur) mean += d.first;
+                    mean /= (double)dur.size();
+                    const size_t nd = dur.size();
+                    const unsigned long long* qm = &p[(size_t)dur[nd / 2].second * 32];
+                    const unsigned long long* qx = &p[(size_t)dur[nd - 1].second * 32];
+                    fprintf(stderr, "[bgx fused prof] last launch, %zu workgroups: duration us min %.1f p50 %.1f mean %.1f "
+                            "p90 %.1f max %.1f; begin skew %.1f us, span %.1f us; lane-steps %llu; rows / tier-2 jobs: "
+                            "median workgroup %llu / %llu, slowest %llu / %llu\n",
+                            nd, dur[0].first, dur[nd / 2].first, mean, dur[(nd * 9) / 10].first, dur[nd - 1].first,
+                            (double)(b_max - b_min) / 100.0, (double)(e_max - b_min) / 100.0, qx[28], qm[26], qm[27],
+                            qx[26], qx[27]);
+                }
             }
             hipFree(e->fprof);
         }

@@ -115,6 +115,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     a.err_flags = e.err_flags;
 
     unsigned long long n_rows = 0, n_fb = 0, n_steps = 0;
+    const unsigned long long wg_begin = PROF ? wall_clock64() : 0ull;   // this launch's span (f.prof)
     // development timers (f.prof): phase sums on thread 0, per-wave sums on lane 0
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tj = 0, tc = 0, tw[4] = {0, 0, 0, 0}, t2c = 0, t3n = 0;
     unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
@@ -454,6 +455,14 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     if (prof) {
         unsigned long long* P = f.prof + (size_t)blockIdx.x * 32;
         if (t == 0) {
+            // the last launch's begin / end clocks, rows and tier-2 jobs of this
+            // workgroup (overwritten per launch: the spread of the workgroups'
+            // durations is what a short launch waits for)
+            P[24] = wg_begin;
+            P[25] = wall_clock64();
+            P[26] = n_rows;
+            P[27] = n_fb;
+            P[28] = n_steps;
             for (int k = 0; k < 6; ++k) atomicAdd(P + k, ph[k]);
             atomicAdd(P + 11, t2c);
             atomicAdd(P + 12, n_fb);
