@@ -114,14 +114,15 @@ def sum_over_ranks(x, world):
     return float(t.item())
 
 
-def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_every, timing, timing_steps=0):
+def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_every, timing, timing_steps=0,
+               desync=0):
     from bgx import Engine
     from bgx import dist as bdist
     w = load_weights()
     if world > 1:
         w = bdist.broadcast_weights(w)
     eng = Engine(lanes=lanes, seed=args.seed, ply=ply, k_top=k_top, lane_base=rank * lanes,
-                 fused=not args.no_fused)
+                 fused=not args.no_fused, balance=not args.no_balance)
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
 
@@ -148,6 +149,11 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
         if pending is not None:
             collect(pending)
 
+    # lanes start together from the reset; `desync` untimed steps
+    # (harvested, and gathered at N > 1, like the timed ones) spread them over
+    # their games so the timed window holds finished episodes, refills and
+    # harvests, then the driver's warmup
+    run(desync)
     run(warmup)
     eng.sync()
     s0 = eng.stats()
@@ -267,7 +273,14 @@ def _pmc(leg, group, key):
 def roofline_fused(d, tm):
     """The fused 1-ply step kernel (one launch = all steps of a step() call):
     the whole path's algorithmic bytes (54 B per movegen job +
-    901 B per evaluated board) and MLP FLOPs over its average launch."""
+    901 B per evaluated board) and MLP FLOPs over its average launch.
+
+    The kernel is not HBM-bound: fusion keeps features and V on chip, so its
+    physical traffic (PMC) is ~1/28 of the algorithmic bytes, and its counters
+    (VALU ~0.5, MFMA ~0.2 busy, ~44 % of wave-cycles waiting) put it on
+    latency: a chain of phases behind workgroup barriers. `bound` says so;
+    achieved / peak / frac stay the algorithmic-bytes figure of the bench
+    contract, with the physical rate and the busy ratios beside it."""
     el = d["elapsed_s"]
     n = max(1, tm["movegen_launches"])
     launch = tm["movegen_ms"] / n
@@ -282,12 +295,21 @@ def roofline_fused(d, tm):
          "unit": "TFLOP/s", "avg_launch_ms": launch, "launches": n,
          "basis": "50,944 FLOP per evaluated board (fp16x2 split: 2x that on the MFMA pipes)"}
     m["frac"] = m["achieved"] / m["peak"]
-    r = {kk: k[kk] for kk in ("bound", "achieved", "peak", "unit", "frac")}
+    r = {kk: k[kk] for kk in ("achieved", "peak", "unit", "frac")}
+    r["bound"] = "latency"
+    r["bound_detail"] = ("VALU/LDS issue of dependent phases behind workgroup barriers (not HBM: physical "
+                         "traffic below; not MFMA: mfma_busy below)")
     r["kernel"] = "bgx::fused_step_kernel (movegen + encode + MLP + select + env step, all steps of a launch)"
+    r["achieved_basis"] = "SURVEY 8d algorithmic bytes (54 B per movegen job + 901 B per evaluated board)"
     # PMC bytes per step of the same workload x the steps of this bench's launches
     per_step, src = _pmc("1ply_fused", "fused", "hbm_bytes_per_step")
     r["traffic"] = per_step * k["steps_per_launch"] if per_step else None
     r["traffic_source"] = src if per_step else None
+    r["physical_gbs"] = r["traffic"] / (launch * 1e-3) / 1e9 if r["traffic"] else None
+    r["physical_frac"] = r["physical_gbs"] / HBM_PEAK_GBS if r["physical_gbs"] else None
+    for key in ("valu_busy", "mfma_busy", "lds_busy", "salu_busy", "wait_frac", "issue_stall_frac", "waves_per_cu"):
+        r[key] = _pmc("1ply_fused", "fused", key)[0]
+    r["mfma_frac_algorithmic"] = m["frac"]
     return r, {"fused_step": k, "fused_step_mfma": m}
 
 
@@ -318,10 +340,13 @@ def roofline_for(d, tm, leg):
     r["kernel"] = (("movegen launch = bgx::movegen_few_kernel + bgx::movegen_block_kernel" if leg == "1ply" else
                     "movegen launches = (few | pool) + bgx::movegen_block_kernel")
                    if dom == "movegen" else "bgx::mlp_kernel")
-    r["traffic"], r["traffic_source"] = _pmc(leg, dom, "hbm_bytes_per_launch") if leg == "2ply_k4" else (None, None)
-    busy, bsrc = _pmc(leg, dom, "valu_busy") if leg == "2ply_k4" else (None, None)
-    if busy is not None:
-        r["valu_busy"], r["valu_busy_source"] = busy, bsrc
+    r["traffic"], r["traffic_source"] = _pmc(leg, dom, "hbm_bytes_per_launch") if leg != "1ply" else (None, None)
+    if r["traffic"]:
+        r["physical_gbs"] = r["traffic"] / (out[dom]["avg_launch_ms"] * 1e-3) / 1e9
+    for key in ("valu_busy", "mfma_busy", "wait_frac", "issue_stall_frac", "waves_per_cu"):
+        v, _src = _pmc(leg, dom, key) if leg != "1ply" else (None, None)
+        if v is not None:
+            r[key] = v
     return r, out
 
 
@@ -347,6 +372,8 @@ def main():
     ap.add_argument("--ply", type=int, default=1)
     ap.add_argument("--k-top", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--desync-steps", type=int, default=300,
+                    help="untimed steps before the warmup so lanes are spread over their games (SURVEY 8d)")
     ap.add_argument("--harvest-every", type=int, default=300,
                     help="steps per bgx_step launch between harvests (<= ring - max_steps)")
     ap.add_argument("--two-ply-steps", type=int, default=100, help="2-ply K=4 leg (configs[4]); 0 = skip")
@@ -361,6 +388,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true",
                     help="1-ply: one launch per phase and step instead of the fused persistent step kernel")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="fused 1-ply: every lane runs exactly the steps of a call (lockstep) instead of the "
+                         "balanced launch (a step(n) call = n x lanes lane-steps, faster workgroups run ahead)")
     ap.add_argument("--timing-steps", type=int, default=200,
                     help="length of the event-timed pass that feeds roofline (2-ply: min(this, 50))")
     args = ap.parse_args()
@@ -390,9 +420,11 @@ def main():
 
     world, rank, local = init_dist()
 
-    def leg(ply, k_top, lanes, steps, warmup, timing_steps, name):
+    def leg(ply, k_top, lanes, steps, warmup, timing_steps, name, desync=None):
+        desync = args.desync_steps if desync is None else desync
         el_, d_, tm_, dtm_, gathered_ = run_engine(args, world, rank, ply, k_top, lanes, steps, warmup,
-                                                   args.harvest_every, timing=True, timing_steps=timing_steps)
+                                                   args.harvest_every, timing=True, timing_steps=timing_steps,
+                                                   desync=desync)
         el_ = max_over_ranks(el_, world)
         per_rank = [int(x) for x in all_ranks(d_["env_steps"], world)]
         roof_, kern_ = roofline_for(dtm_, tm_, name)
@@ -403,7 +435,7 @@ def main():
                 "value_rows_per_s": sum_over_ranks(d_["value_rows"], world) / el_,
                 "movegen_jobs_per_s": sum_over_ranks(d_["movegen_jobs"], world) / el_,
                 "fallback_jobs": int(sum_over_ranks(d_["fallback_jobs"], world)),
-                "roofline": roof_, "kernels": kern_}
+                "roofline": roof_, "kernels": kern_, "desync_steps": desync}
         if world > 1:
             out_["gathered_episodes"], out_["gathered_records"] = gathered_
         return out_, d_
@@ -436,9 +468,11 @@ def main():
                                        if args.lanes == 8192 else "")),
                        "lanes_per_gpu": args.lanes, "lanes_total": args.lanes * world, "ply": args.ply,
                        "harvest_every": args.harvest_every,
-                       "engine": "fused step kernel" if args.ply == 1 and not args.no_fused else "phased launches",
+                       "engine": ("fused step kernel" + ("" if args.no_balance else ", balanced launches")
+                                  if args.ply == 1 and not args.no_fused else "phased launches"),
                        "parallelism": (f"lanes sharded x{world}, RCCL episode gather to rank 0 "
                                        f"({BACKEND})" if world > 1 else "single GPU")},
+            "desync_steps": head["desync_steps"],
             "world_size": world, "env_steps_per_rank": head["env_steps_per_rank"],
             "decisions_per_s": head["decisions_per_s"], "episodes_per_s": head["episodes_per_s"],
             "value_rows_per_s": head["value_rows_per_s"], "fallback_jobs": head["fallback_jobs"],

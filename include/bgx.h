@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 6
+#define BGX_ABI_VERSION 7
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -38,6 +38,32 @@ extern "C" {
 
 int bgx_abi_version(void);
 const char* bgx_last_error(void);
+
+/* Input domain of the stateless entry points below (bgx_movegen, bgx_encode,
+ * bgx_value_boards, bgx_two_ply*): the boards a game can reach, as the
+ * reference's ImmutableBoard holds them (board/immutable_board.py:16-24) —
+ * every count <= 15, at most 15 checkers per player (points + bar + off), no
+ * point held by both players — player 0 / 1 and dice 1..6 (randint(1, 7),
+ * environments/backgammon_env.py:310-311). The check runs on the device (the
+ * inputs stay device pointers); an input outside it makes the call return
+ * BGX_E_ARG with the offending bits and the first bad index in the message,
+ * before any output is written. These calls therefore synchronize `stream`
+ * once (the reference's move_checker only prints a warning on an invalid move,
+ * immutable_board.py:197-236; here nothing is computed for such a batch). */
+#define BGX_BADF_SHARED_POINT 1u   /* a point holds checkers of both players */
+#define BGX_BADF_TOTAL 2u          /* a player has more than 15 checkers */
+#define BGX_BADF_VALUE 4u          /* a board byte above 15 */
+#define BGX_BADF_DICE 8u           /* a die outside 1..6 */
+#define BGX_BADF_PLAYER 16u        /* a player byte other than 0 / 1 */
+
+/* The same check on its own: *h_flags = OR of BGX_BADF_* over the n inputs,
+ * *h_first_bad = the lowest offending index (-1 if none). d_player and d_dice
+ * may be NULL (not checked). Returns BGX_OK whatever the flags; synchronizes. */
+int bgx_check_boards(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t* d_dice, int n,
+                     uint32_t* h_flags, int32_t* h_first_bad, void* stream);
+/* The same rule on host arrays (no device; the host variant of the check). */
+int bgx_check_boards_host(const uint8_t* h_boards, const uint8_t* h_player, const uint8_t* h_dice, int n,
+                          uint32_t* h_flags, int32_t* h_first_bad);
 
 /* ---------------- stateless parity entry points ---------------- */
 
@@ -112,6 +138,14 @@ typedef struct bgx_config {
                                MLP, select, step fused; same results as 0 = one launch per phase) */
     int reply_sample;       /* 2-ply: 0 (default) = exact mode; 50 = the reference's random.sample of 50
                                replies for 1-1 / 2-2 / 3-3 (two_ply.py:119-121), keyed by seed + step */
+    int balance;            /* fused 1-ply, lanes <= 32 x CUs: 1 = bgx_step(n) runs n x lanes lane-steps in
+                               total instead of n steps of every lane: the workgroups whose lanes step
+                               faster run ahead (a lane may run up to n + n/4 + 4 steps in a call, at most
+                               ring - max_steps), so a launch does not wait for its slowest workgroup.
+                               Each lane's game is unchanged (dice and sampling keyed by lane and its own
+                               counters), as the reference's 7 workers each run at their own pace
+                               (main.py:86-91); only how far each lane got at a harvest differs.
+                               0 (default) = lockstep. */
 } bgx_config;
 
 void bgx_config_default(bgx_config* cfg);
@@ -138,7 +172,8 @@ int bgx_set_weights(bgx_engine* e, const float* h_W1, const float* h_b1, const f
 int bgx_engine_set_dice(bgx_engine* e, const uint8_t* h_dice, int per_lane);
 
 /* Advance every lane by n_steps env steps (one BackgammonEnv.step each,
- * passes included; finished games are recorded and the lane restarts). */
+ * passes included; finished games are recorded and the lane restarts); with
+ * cfg.balance, n_steps x lanes lane-steps in total (bgx_get_stats counts them). */
 int bgx_step(bgx_engine* e, int n_steps, void* stream);
 /* Wait for the engine's stream; reports device-side overflow flags. */
 int bgx_sync(bgx_engine* e);

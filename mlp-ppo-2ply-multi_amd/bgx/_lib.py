@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("BGX_LIB", os.path.join(_HERE, "libbgx.so"))
 c_int, c_float, c_double, c_u64, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                              ctypes.c_uint64, ctypes.c_void_p)
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class BgxError(RuntimeError):
@@ -34,7 +34,7 @@ class Config(ctypes.Structure):
         ("lanes", c_int), ("lane_base", c_int), ("seed", c_u64), ("ply", c_int), ("k_top", c_int),
         ("alpha", c_float), ("beta", c_float), ("max_steps", c_int), ("max_legal", c_int),
         ("ring", c_int), ("ep_cap", c_int), ("cand_per_lane", c_int), ("reply_per_lane", c_int),
-        ("greedy", c_int), ("fused", c_int), ("reply_sample", c_int),
+        ("greedy", c_int), ("fused", c_int), ("reply_sample", c_int), ("balance", c_int),
     ]
 
 
@@ -52,6 +52,10 @@ class Stats(ctypes.Structure):
 SIGNATURES = {
     "bgx_abi_version": (c_int, []),
     "bgx_last_error": (ctypes.c_char_p, []),
+    "bgx_check_boards": (c_int, [c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.POINTER(ctypes.c_int32), c_void_p]),
+    "bgx_check_boards_host": (c_int, [c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(ctypes.c_uint32),
+                                      ctypes.POINTER(ctypes.c_int32)]),
     "bgx_movegen": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "bgx_encode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "bgx_net_create": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_void_p)]),

@@ -35,7 +35,7 @@ class Harvest:
 class Engine:
     def __init__(self, lanes=4096, seed=0, ply=1, k_top=4, device=None, lane_base=0, alpha=1.0,
                  beta=0.9, max_steps=300, max_legal=500, ring=1024, ep_cap=0, cand_per_lane=256,
-                 reply_per_lane=0, greedy=False, fused=True, reply_sample=0):
+                 reply_per_lane=0, greedy=False, fused=True, reply_sample=0, balance=False):
         require_cuda()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         cfg = Config()
@@ -47,6 +47,7 @@ class Engine:
         cfg.greedy = 1 if greedy else 0
         cfg.fused = 1 if fused else 0   # 1-ply: one persistent launch per step() call
         cfg.reply_sample = int(reply_sample)   # 2-ply: 0 exact, 50 = two_ply.py:119-121 random.sample
+        cfg.balance = 1 if balance else 0   # fused 1-ply: step(n) = n x lanes lane-steps (include/bgx.h)
         self.cfg = cfg
         self.lanes = int(lanes)
         self.fused = bool(fused) and int(ply) == 1
@@ -93,7 +94,8 @@ class Engine:
               "bgx_engine_set_dice")
 
     def step(self, n=1, stream=None):
-        """Advance every lane by n env steps (asynchronous on the stream)."""
+        """Advance every lane by n env steps (asynchronous on the stream);
+        balance=True: n x lanes lane-steps in total, faster lanes run ahead."""
         check(lib().bgx_step(self._h, int(n), stream_handle(stream)), "bgx_step")
 
     def sync(self):

@@ -42,6 +42,23 @@ def movegen(boards, player, dice, cap: int = 512, stream=None):
     return out, cnt
 
 
+BAD_BITS = {1: "a point held by both players", 2: "more than 15 checkers of a player",
+            4: "a count above 15", 8: "a die outside 1..6", 16: "a player not 0/1"}
+
+
+def check_boards(boards, player=None, dice=None, stream=None):
+    """The input-domain check of the stateless ops (include/bgx.h BGX_BADF_*)
+    on the device: returns (flags, first bad index or -1)."""
+    boards = _u8(boards).view(-1, 52)
+    require_cuda(boards)
+    player = None if player is None else _u8(player).view(-1)
+    dice = None if dice is None else _u8(dice).view(-1, 2)
+    f, first = ctypes.c_uint32(0), ctypes.c_int32(-1)
+    check(lib().bgx_check_boards(ptr(boards), ptr(player), ptr(dice), boards.shape[0], ctypes.byref(f),
+                                 ctypes.byref(first), stream_handle(stream)), "bgx_check_boards")
+    return int(f.value), int(first.value)
+
+
 def encode(boards, player, layout: int = 0, stream=None):
     boards, player = _u8(boards).view(-1, 52), _u8(player).view(-1)
     require_cuda(boards, player)

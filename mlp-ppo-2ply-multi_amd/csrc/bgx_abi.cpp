@@ -14,9 +14,11 @@
 #include <exception>
 #include <new>
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "bgx.h"
+#include "bgx_domain.h"
 #include "bgx_kernels.h"
 
 namespace {
@@ -60,8 +62,6 @@ struct bgx_net {
     uint4* wfrag = nullptr;   // split-fp16 MFMA fragments
     float* rowc = nullptr;    // [128] w2
     float feat_scale = 1.0f;  // 2^-e: features scaled so the accumulator is the exp2 argument
-    uint32_t* scratch = nullptr;   // packed boards for bgx_value_boards
-    int scratch_n = 0;
 };
 
 // Split-fp16 fragments (see bgx_mlp.hip header for the scheme). Returns e.
@@ -136,7 +136,8 @@ struct bgx_engine {
     float* V = nullptr;
     int32_t* cand_off = nullptr;
     int32_t* cand_cnt = nullptr;
-    unsigned* ctr = nullptr;   // [3] ep, [4] err; per-step (zeroed each step): [8] flat, [9] reply, [10] ovf, [11] ovf2
+    unsigned* ctr = nullptr;   // [3] ep, [4] err; per-step (zeroed each step): [8] flat, [9] reply, [10] ovf, [11] ovf2;
+                               // [12..13] balanced-launch lane-step counter
     unsigned long long* stats = nullptr;
     int32_t* sel = nullptr;
     uint32_t* sel_rows = nullptr;
@@ -184,6 +185,13 @@ struct bgx_engine {
 
 namespace {
 constexpr int C_EP = 3, C_ERR = 4, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
+constexpr int C_BUDGET = 12;   // [12..13]: the balanced fused launch's lane-step counter (u64)
+}
+
+static int flag_error(unsigned f) {
+    return fail(f & BGX_ERRF_WAIT_BOUND ? BGX_E_STATE : BGX_E_CAPACITY,
+                "device flags 0x%x (1 flat rows, 2 overflow list, 4 fallback workspace, 8 experience ring, "
+                "16 episode list, 32 scripted dice: capacity; 64 an intra-workgroup wait hit its bound: state)", f);
 }
 
 static int check_flags(bgx_engine* e) {
@@ -191,8 +199,7 @@ static int check_flags(bgx_engine* e) {
     HIP_TRY(hipMemcpy(&f, e->ctr + C_ERR, 4, hipMemcpyDeviceToHost));
     if (f) {
         HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
-        return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
-                    "workspace, 8 experience ring, 16 episode list, 32 scripted dice)", f);
+        return flag_error(f);
     }
     return BGX_OK;
 }
@@ -214,10 +221,175 @@ static int guarded(const char* what, F&& body) noexcept {
     }
 }
 
+// ---------------------------------------------------------------- stateless-call scratch
+// The stateless entry points need a few device words (validation flags,
+// movegen overflow counters), an overflow list, a fallback workspace and (for
+// bgx_value_boards) packed boards. Each call leases one scratch set from a
+// per-device pool: a set is handed out only when no call holds it and the
+// stream work of its last user has finished (an event recorded at release),
+// so calls from several host threads or on several streams never share one.
+// Sets are kept for reuse; the pool grows to the peak number of calls in flight.
+namespace {
+
+struct Scratch {
+    int dev = -1;
+    bool busy = false;
+    hipEvent_t done = nullptr;
+    unsigned* words = nullptr;     // [16]: [0..1] validation flags, [2] ovf count, [3] err flags
+    uint32_t* h_words = nullptr;   // pinned host copy of words[0..1]
+    int32_t* ovf = nullptr;        // movegen overflow list (lazy)
+    uint32_t* ws = nullptr;        // movegen fallback workspace (lazy)
+    uint32_t* packed = nullptr;    // bgx_value_boards packed boards (lazy, grows)
+    size_t packed_n = 0;
+};
+
+constexpr int SC_OVF_CAP = 1 << 16, SC_WS_WAVES = 256, SC_WS_SLOTS = 16384;
+
+std::mutex g_pool_mu;
+std::vector<Scratch*> g_pool;
+
+// hipSetDevice to the device holding `p` (a device pointer) for the scope; the
+// caller's current device is restored at the end
+struct DeviceScope {
+    int prev = -1;
+    int dev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(const void* p) {
+        err = hipGetDevice(&prev);
+        if (err != hipSuccess) return;
+        dev = prev;
+        hipPointerAttribute_t at{};
+        if (p && hipPointerGetAttributes(&at, p) == hipSuccess && at.device >= 0 && at.device != prev) {
+            err = hipSetDevice(at.device);
+            dev = at.device;
+        }
+        (void)hipGetLastError();   // a host pointer's attribute query is not an error here
+    }
+    ~DeviceScope() {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct Lease {
+    Scratch* sc = nullptr;
+    hipStream_t stream = nullptr;
+    ~Lease() {
+        if (!sc) return;
+        (void)hipEventRecord(sc->done, stream);
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        sc->busy = false;
+    }
+};
+
+int lease_scratch(hipStream_t stream, Lease& L) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (Scratch* sc : g_pool) {
+            if (sc->dev != dev || sc->busy || hipEventQuery(sc->done) != hipSuccess) continue;
+            sc->busy = true;
+            L.sc = sc;
+            L.stream = stream;
+            return BGX_OK;
+        }
+    }
+    Scratch* sc = new Scratch();
+    sc->dev = dev;
+    sc->busy = true;
+    if (dalloc(&sc->words, 16)) {
+        delete sc;
+        return BGX_E_HIP;
+    }
+    if (hipHostMalloc((void**)&sc->h_words, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&sc->done, hipEventDisableTiming) != hipSuccess) {
+        hipFree(sc->words);
+        if (sc->h_words) hipHostFree(sc->h_words);
+        delete sc;
+        return fail(BGX_E_HIP, "scratch: pinned buffer / event creation failed");
+    }
+    HIP_TRY(hipMemset(sc->words, 0, 64));
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pool.push_back(sc);
+    }
+    L.sc = sc;
+    L.stream = stream;
+    return BGX_OK;
+}
+
+int lease_movegen_space(Scratch* sc) {
+    if (!sc->ovf && dalloc(&sc->ovf, SC_OVF_CAP)) return BGX_E_HIP;
+    if (!sc->ws && dalloc(&sc->ws, (size_t)SC_WS_WAVES * 5 * SC_WS_SLOTS)) return BGX_E_HIP;
+    return BGX_OK;
+}
+
+// the input-domain check (include/bgx.h, BGX_BADF_*): flags into the lease's
+// words, copied to pinned memory, one stream synchronization
+int check_domain(Scratch* sc, const uint8_t* boards, const uint8_t* player, const uint8_t* dice, int n,
+                 hipStream_t s, uint32_t* flags, int32_t* first) {
+    HIP_TRY(bgx_launch_validate(boards, player, dice, n, sc->words, s));
+    HIP_TRY(hipMemcpyAsync(sc->h_words, sc->words, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *flags = sc->h_words[0];
+    *first = sc->h_words[0] ? (int32_t)sc->h_words[1] : -1;
+    return BGX_OK;
+}
+
+int require_domain(const char* what, Scratch* sc, const uint8_t* boards, const uint8_t* player,
+                   const uint8_t* dice, int n, hipStream_t s) {
+    uint32_t f = 0;
+    int32_t first = -1;
+    if (int rc = check_domain(sc, boards, player, dice, n, s, &f, &first)) return rc;
+    if (f)
+        return fail(BGX_E_ARG,
+                    "%s: input %d is outside the board domain (bits 0x%x: 1 a point held by both players, 2 more "
+                    "than 15 checkers of a player, 4 a count above 15, 8 a die outside 1..6, 16 a player not 0/1)",
+                    what, first, f);
+    return BGX_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int bgx_abi_version(void) { return BGX_ABI_VERSION; }
 const char* bgx_last_error(void) { return g_err.c_str(); }
+
+int bgx_check_boards_host(const uint8_t* h_boards, const uint8_t* h_player, const uint8_t* h_dice, int n,
+                          uint32_t* h_flags, int32_t* h_first_bad) {
+    return guarded("bgx_check_boards_host", [&]() -> int {
+        if (n < 0 || !h_flags || !h_first_bad || (n > 0 && !h_boards))
+            return fail(BGX_E_ARG, "bgx_check_boards_host: bad arguments (n=%d)", n);
+        uint32_t f = 0;
+        int32_t first = -1;
+        for (int i = 0; i < n; ++i) {
+            const unsigned b = bgx::domain_bits(h_boards + (size_t)i * 52, h_player ? (int)h_player[i] : -1,
+                                                h_dice ? h_dice + 2 * (size_t)i : nullptr);
+            if (b && first < 0) first = i;
+            f |= b;
+        }
+        *h_flags = f;
+        *h_first_bad = first;
+        return BGX_OK;
+    });
+}
+
+int bgx_check_boards(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t* d_dice, int n,
+                     uint32_t* h_flags, int32_t* h_first_bad, void* stream) {
+    return guarded("bgx_check_boards", [&]() -> int {
+        if (n < 0 || !h_flags || !h_first_bad || (n > 0 && !d_boards))
+            return fail(BGX_E_ARG, "bgx_check_boards: bad arguments (n=%d)", n);
+        *h_flags = 0;
+        *h_first_bad = -1;
+        if (n == 0) return BGX_OK;
+        DeviceScope ds(d_boards);
+        HIP_TRY(ds.err);
+        Lease L;
+        if (int rc = lease_scratch((hipStream_t)stream, L)) return rc;
+        return check_domain(L.sc, d_boards, d_player, d_dice, n, (hipStream_t)stream, h_flags, h_first_bad);
+    });
+}
 
 int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t* d_dice, int n,
                 uint8_t* d_out_boards, int32_t* d_out_count, int cap, void* stream) {
@@ -226,20 +398,14 @@ int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t*
         if (n == 0) return BGX_OK;
         if (!d_boards || !d_player || !d_dice || !d_out_count || (cap > 0 && !d_out_boards))
             return fail(BGX_E_ARG, "bgx_movegen: null pointer");
-        // per-call scratch for the overflow path (kept across calls)
-        static unsigned* ctr = nullptr;
-        static int32_t* ovf = nullptr;
-        static uint32_t* ws = nullptr;
-        static int cur_dev = -1;
-        int dev = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        const int ovf_cap = 1 << 16, ws_waves = 256, ws_slots = 16384;
-        if (!ctr || cur_dev != dev) {
-            if (dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
-                return BGX_E_HIP;
-            HIP_TRY(hipMemset(ctr, 0, 32));
-            cur_dev = dev;
-        }
+        DeviceScope ds(d_boards);
+        HIP_TRY(ds.err);
+        hipStream_t s = (hipStream_t)stream;
+        Lease L;
+        if (int rc = lease_scratch(s, L)) return rc;
+        if (int rc = require_domain("bgx_movegen", L.sc, d_boards, d_player, d_dice, n, s)) return rc;
+        if (int rc = lease_movegen_space(L.sc)) return rc;
+        unsigned* ctr = L.sc->words + 2;   // [0] overflow count, [1] error flags
         bgx::MovegenArgs a{};
         a.n_jobs = n;
         a.in_mode = bgx::IN_U8;
@@ -251,14 +417,14 @@ int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t*
         a.out_u8 = d_out_boards;
         a.out_count = d_out_count;
         a.ovf_count = ctr;
-        a.ovf_list = ovf;
-        a.ovf_cap = ovf_cap;
-        a.ws_global = ws;
-        a.ws_waves = ws_waves;
-        a.ws_slots = ws_slots;
-        a.ws_words_per_wave = (size_t)5 * ws_slots;
+        a.ovf_list = L.sc->ovf;
+        a.ovf_cap = SC_OVF_CAP;
+        a.ws_global = L.sc->ws;
+        a.ws_waves = SC_WS_WAVES;
+        a.ws_slots = SC_WS_SLOTS;
+        a.ws_words_per_wave = (size_t)5 * SC_WS_SLOTS;
         a.err_flags = ctr + 1;
-        HIP_TRY(bgx_launch_movegen(&a, (hipStream_t)stream));
+        HIP_TRY(bgx_launch_movegen(&a, s));
         return BGX_OK;
     });
 }
@@ -269,6 +435,11 @@ int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d
         if (n < 0 || (layout != 0 && layout != 1)) return fail(BGX_E_ARG, "bgx_encode: n=%d layout=%d", n, layout);
         if (n == 0) return BGX_OK;
         if (!d_boards || !d_player || !d_out) return fail(BGX_E_ARG, "bgx_encode: null pointer");
+        DeviceScope ds(d_boards);
+        HIP_TRY(ds.err);
+        Lease L;
+        if (int rc = lease_scratch((hipStream_t)stream, L)) return rc;
+        if (int rc = require_domain("bgx_encode", L.sc, d_boards, d_player, nullptr, n, (hipStream_t)stream)) return rc;
         HIP_TRY(bgx_launch_encode(d_boards, d_player, n, d_out, layout, (hipStream_t)stream));
         return BGX_OK;
     });
@@ -342,7 +513,6 @@ int bgx_net_destroy(bgx_net* n) {
         hipFree(n->w2);
         hipFree(n->wfrag);
         hipFree(n->rowc);
-        hipFree(n->scratch);
         delete n;
         return BGX_OK;
     });
@@ -363,23 +533,30 @@ int bgx_value_boards(const bgx_net* cnet, const uint8_t* d_boards, const uint8_t
         bgx_net* net = const_cast<bgx_net*>(cnet);
         if (!net || n < 0) return fail(BGX_E_ARG, "bgx_value_boards: bad arguments");
         if (n == 0) return BGX_OK;
-        if (net->scratch_n < n) {
-            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-            hipFree(net->scratch);
-            net->scratch = nullptr;
-            if (dalloc(&net->scratch, (size_t)n * 8)) return BGX_E_HIP;
-            net->scratch_n = n;
+        if (!d_boards || !d_player || !d_out) return fail(BGX_E_ARG, "bgx_value_boards: null pointer");
+        DeviceScope ds(d_boards);
+        HIP_TRY(ds.err);
+        hipStream_t s = (hipStream_t)stream;
+        Lease L;
+        if (int rc = lease_scratch(s, L)) return rc;
+        if (int rc = require_domain("bgx_value_boards", L.sc, d_boards, d_player, nullptr, n, s)) return rc;
+        if (L.sc->packed_n < (size_t)n) {   // the lease's last user has finished (lease_scratch)
+            hipFree(L.sc->packed);
+            L.sc->packed = nullptr;
+            L.sc->packed_n = 0;
+            if (dalloc(&L.sc->packed, (size_t)n * 8)) return BGX_E_HIP;
+            L.sc->packed_n = (size_t)n;
         }
-        HIP_TRY(bgx_launch_pack(d_boards, d_player, n, net->scratch, (hipStream_t)stream));
+        HIP_TRY(bgx_launch_pack(d_boards, d_player, n, L.sc->packed, s));
         bgx::MlpArgs m{};
-        m.rows = net->scratch;
+        m.rows = L.sc->packed;
         m.n_rows = n;
         m.out = d_out;
         m.wfrag = net->wfrag;
         m.rowc = net->rowc;
         m.b2 = net->b2;
         m.feat_scale = net->feat_scale;
-        HIP_TRY(bgx_launch_mlp(&m, (hipStream_t)stream));
+        HIP_TRY(bgx_launch_mlp(&m, s));
         return BGX_OK;
     });
 }
@@ -399,7 +576,14 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
             return fail(BGX_E_ARG, "bgx_two_ply_sampled: sample_k=%d (0 = exact, 5..1024)", sample_k);
         if (n == 0) return BGX_OK;
         if (!d_boards || !d_opponent || !d_out) return fail(BGX_E_ARG, "bgx_two_ply: null pointer");
+        DeviceScope ds(d_boards);
+        HIP_TRY(ds.err);
         hipStream_t s = (hipStream_t)stream;
+        {
+            Lease L;
+            if (int rc = lease_scratch(s, L)) return rc;
+            if (int rc = require_domain("bgx_two_ply", L.sc, d_boards, d_opponent, nullptr, n, s)) return rc;
+        }
         const int jobs = n * 21;
         const int cap = jobs * 768;   // >= any reply count per (board, roll)
         uint8_t* mover = nullptr;
@@ -899,6 +1083,13 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.ws_words_per_block = (size_t)5 * e->ws_slots;
     f.force_tier = e->force_tier;
     f.lanes_per_wg = e->fused_fl;
+    if (e->cfg.balance) {   // n_steps x lanes lane-steps; a lane runs at most n + n/4 + 4 (ring headroom)
+        f.budget = (long long)n_steps * (long long)e->cfg.lanes;
+        const int headroom = e->cfg.ring - e->cfg.max_steps;
+        const int cap = n_steps + n_steps / 4 + 4;
+        f.n_cap = cap < headroom ? cap : headroom;
+        f.budget_ctr = (unsigned long long*)(e->ctr + C_BUDGET);
+    }
     if (e->prof_enabled) {
         if (!e->fprof) {
             if (dalloc(&e->fprof, (size_t)1024 * 32)) return BGX_E_HIP;
@@ -985,8 +1176,7 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
         const uint32_t flags = e->h_info[2];
         if (flags) {
             HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
-            return fail(BGX_E_CAPACITY, "device overflow flags 0x%x (1 flat rows, 2 overflow list, 4 fallback "
-                        "workspace, 8 experience ring, 16 episode list, 32 scripted dice)", flags);
+            return flag_error(flags);
         }
         out->n_episodes = (int)e->h_info[0];
         out->n_records = (int)e->h_info[1];

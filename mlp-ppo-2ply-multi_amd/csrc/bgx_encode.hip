@@ -12,6 +12,7 @@
 // float4 of the flat [n][198] output (fully coalesced dwordx4 stores); the
 // board bytes it needs come through L1/L2.
 #include "bgx_device.h"
+#include "bgx_domain.h"
 #include "bgx_kernels.h"
 
 namespace bgx {
@@ -102,7 +103,35 @@ __global__ __launch_bounds__(256) void unpack_kernel(const uint32_t* __restrict_
     for (int k = 0; k < 13; ++k) d[k] = o[k];
 }
 
+// Input-domain check of the stateless entry points (one thread per board;
+// bgx_domain.h): flags[0] |= BGX_BADF_* bits, flags[1] = lowest offending
+// index (atomicMin; the launcher presets ~0).
+__global__ __launch_bounds__(256) void validate_kernel(const uint8_t* __restrict__ boards,
+                                                       const uint8_t* __restrict__ player,
+                                                       const uint8_t* __restrict__ dice, int n,
+                                                       unsigned* __restrict__ flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned bad = domain_bits(boards + (size_t)i * 52, player ? (int)player[i] : -1,
+                                     dice ? dice + 2 * (size_t)i : nullptr);
+    if (bad) {
+        atomicOr(&flags[0], bad);
+        atomicMin(&flags[1], (unsigned)i);
+    }
+}
+
 }  // namespace bgx
+
+extern "C" hipError_t bgx_launch_validate(const uint8_t* boards, const uint8_t* player, const uint8_t* dice,
+                                          int n, unsigned* flags, hipStream_t stream) {
+    const unsigned init[2] = {0u, 0xFFFFFFFFu};
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)flags, init[0], 1, stream);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(flags + 1), init[1], 1, stream);
+    if (e != hipSuccess || n <= 0) return e;
+    hipLaunchKernelGGL(bgx::validate_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, boards, player, dice, n,
+                       flags);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t bgx_launch_encode(const uint8_t* boards, const uint8_t* player, int n,
                                         float* out, int layout, hipStream_t stream) {

@@ -48,6 +48,7 @@ template <int FL> struct FusedTail {
     int cnt[FL];                    // lane's full candidate count this step (-1: redo in tier 2)
     int next[2];                    // tier-1 job counters, alternating by step parity
     int bdone;                      // last-round lanes stepped so far (this group; see OVL)
+    int go[2];                      // step s runs iff go[s & 1] (the balanced launch's tickets)
     int pre[FL + 1];                // MLP row prefix over the lanes
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
@@ -141,9 +142,22 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             T.bdone = 0;
         }
         const int na = nlive < NA ? nlive : NA, nbl = nlive - na;   // lanes stepped before / in the last round
-        n_steps += (unsigned long long)nlive * (unsigned long long)f.n_steps;
+        // step s runs iff ticket(s): lockstep, s < n_steps; balanced, s < n_cap and
+        // the launch's lane-step total before this workgroup-step is below the
+        // budget (thread 0 takes step s + 1's ticket while step s runs; the barrier
+        // after tier 1 publishes it)
+        auto ticket = [&](int s) -> int {
+            if (f.budget <= 0) return s < f.n_steps;
+            if (s >= f.n_cap) return 0;
+            const unsigned long long old = atomicAdd(f.budget_ctr, (unsigned long long)nlive);
+            return old < (unsigned long long)f.budget;
+        };
+        if (t == 0) T.go[0] = ticket(0);
         __syncthreads();
-        for (int step = 0; step < f.n_steps; ++step) {
+        const int n_iter = f.budget > 0 ? f.n_cap : f.n_steps;
+        for (int step = 0; step < n_iter && T.go[step & 1]; ++step) {
+            if (t == 0) T.go[(step + 1) & 1] = ticket(step + 1);
+            n_steps += (unsigned long long)nlive;
             // ---- 1. tier-1 movegen of the wave's lanes in its slice
             if (prof && t == 0) tc = wall_clock64();
             {
@@ -191,8 +205,18 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             // is stepped by a wave that has no barrier ahead of it
                             const int target = step * nbl;
                             const unsigned long long b0 = prof ? wall_clock64() : 0ull;
-                            while (__hip_atomic_load(&T.bdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+                            // bounded: the lanes' waves have no barrier ahead, so
+                            // the wait ends; if a change ever breaks that, the bound turns the hang
+                            // into BGX_E_STATE at bgx_sync instead of a stuck GPU
+                            for (unsigned spin = 0;
+                                 __hip_atomic_load(&T.bdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target;
+                                 ++spin) {
+                                if (spin >= (1u << 24)) {
+                                    if (l == 0) atomicOr(e.err_flags, BGX_ERRF_WAIT_BOUND);
+                                    break;
+                                }
                                 __builtin_amdgcn_s_sleep(1);
+                            }
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                             if (prof) twb += wall_clock64() - b0;
                             const bool inb = l >= na && l < nlive;
@@ -445,7 +469,9 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 if (prof) tw[3] += wall_clock64() - s1;
                 }
             }
-            if (!OVL || step + 1 == f.n_steps) __syncthreads();
+            // the next step's ticket (written before this step's first barrier):
+            // the OVL round's lanes are finished by a barrier before the group ends
+            if (!OVL || !T.go[(step + 1) & 1]) __syncthreads();
             tick(4);
             if (prof && t == 0) ph[5] += 1;
         }
@@ -530,16 +556,24 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
     int blocks = groups < n_cu ? groups : n_cu;
     if (blocks > args->ws_blocks) blocks = args->ws_blocks;
     const dim3 g(blocks), b(64 * (fl == 32 ? bgx::FCfg<32>::NW : bgx::FCfg<16>::NW));
+    bgx::FusedArgs a = *args;
+    // balanced only when every workgroup owns one lane group (a workgroup that
+    // walks several groups would spend the budget on its first ones)
+    if (a.budget > 0 && (groups > blocks || !a.budget_ctr || a.n_cap < a.n_steps)) a.budget = 0;
+    if (a.budget > 0) {
+        const hipError_t e = hipMemsetAsync(a.budget_ctr, 0, sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
     if (fl == 32) {
-        if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 32>), g, b, bgx::FCfg<32>::LDS, stream, *args);
+        if (a.prof)
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 32>), g, b, bgx::FCfg<32>::LDS, stream, a);
         else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 32>), g, b, bgx::FCfg<32>::LDS, stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 32>), g, b, bgx::FCfg<32>::LDS, stream, a);
     } else {
-        if (args->prof)
-            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 16>), g, b, bgx::FCfg<16>::LDS, stream, *args);
+        if (a.prof)
+            hipLaunchKernelGGL((bgx::fused_step_kernel<true, 16>), g, b, bgx::FCfg<16>::LDS, stream, a);
         else
-            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 16>), g, b, bgx::FCfg<16>::LDS, stream, *args);
+            hipLaunchKernelGGL((bgx::fused_step_kernel<false, 16>), g, b, bgx::FCfg<16>::LDS, stream, a);
     }
     return hipGetLastError();
 }

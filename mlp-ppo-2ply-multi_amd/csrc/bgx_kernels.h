@@ -3,12 +3,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bgx.h"   // BGX_BADF_* (input-domain bits)
+
 #define BGX_ERRF_FLAT_OVERFLOW 1u       // flat reply buffer too small
 #define BGX_ERRF_OVF_LIST 2u            // overflow job list too small
 #define BGX_ERRF_FALLBACK_OVERFLOW 4u   // a job outgrew the global workspace
 #define BGX_ERRF_RING_OVERFLOW 8u       // experience ring overwritten before harvest
 #define BGX_ERRF_EPISODE_LIST 16u       // finished-episode list full
 #define BGX_ERRF_DICE_EXHAUSTED 32u     // a lane read past its scripted dice (bgx_engine_set_dice)
+#define BGX_ERRF_WAIT_BOUND 64u         // an intra-workgroup wait hit its iteration bound (reported as BGX_E_STATE)
 
 namespace bgx {
 
@@ -145,6 +148,14 @@ struct FusedArgs {
     unsigned long long* prof;    // development (BGX_FUSED_PROF): [gridDim.x][16] phase clocks, or null
     int lanes_per_wg;            // 16 or 32 game lanes per workgroup; 0: the launcher picks (32 when
                                  //   every CU still gets a workgroup)
+    // balanced launch (bgx_config.balance): each workgroup-step takes a ticket of
+    // its lanes from *budget_ctr (zeroed per launch) and steps while the running
+    // total is below `budget` lane-steps, at most n_cap steps; budget <= 0: every
+    // lane runs exactly n_steps (lockstep). The launcher balances only when each
+    // workgroup owns one lane group.
+    long long budget;
+    int n_cap;
+    unsigned long long* budget_ctr;
 };
 
 // TD(0) trainer (bgx_train.hip): one launch over n_eps episodes of compact
@@ -168,6 +179,9 @@ extern "C" {
 hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream_t stream);
 hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t stream);
 hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t stream);
+// input-domain check (flags[0] = BGX_BADF_* bits, flags[1] = first bad index)
+hipError_t bgx_launch_validate(const uint8_t* boards, const uint8_t* player, const uint8_t* dice, int n,
+                               unsigned* flags, hipStream_t stream);
 hipError_t bgx_launch_encode(const uint8_t* boards, const uint8_t* player, int n, float* out,
                              int layout, hipStream_t stream);
 hipError_t bgx_launch_value_f32(const float* x, int n, const float* W1, const float* b1,

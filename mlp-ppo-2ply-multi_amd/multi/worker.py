@@ -1,14 +1,18 @@
 """Worker / worker_function (src/multi/worker.py:17-179) on MI355X lanes.
 
 The reference spawns 7 CPU processes (src/main.py:86-91), each playing one
-game at a time. Here worker `worker_id` drives one bgx.Engine on GPU
-`worker_id` (ids beyond the visible GPU count return immediately, so the
-reference's hard-coded 7 workers map onto the node's GPUs), stepping
-thousands of lanes and putting every finished Episode on the queue exactly as
+game at a time. Here worker `worker_id` drives one bgx.Engine per GPU it is
+given (gpus_for_worker: GPU g goes to worker g mod 7, so the reference's
+hard-coded 7 workers cover all 8 GPUs of a node — worker 0 drives GPUs 0 and 7;
+workers without a GPU return immediately), stepping thousands of lanes per
+GPU and putting every finished Episode on the queue exactly as
 play_episode/run do (worker.py:47-76). Parameters are re-read when the
 version advances (worker.py:66-76), at every harvest.
 
-Knobs (environment): BGX_LANES (4096), BGX_PLY (1), BGX_K_TOP (4),
+Knobs (environment): BGX_WORKERS (7: main.py:86's worker count),
+BGX_GPU_MAP (explicit GPUs per worker id: "0;1;2;3;4;5;6,7" = worker 6 drives
+GPUs 6 and 7), BGX_LANES (4096 per GPU), BGX_PLY (1), BGX_K_TOP (4),
+BGX_BALANCE (1: balanced fused launches, include/bgx.h bgx_config.balance),
 BGX_STEPS_PER_HARVEST (100), BGX_MAX_PENDING (2000 episodes queued before the
 engine pauses: the queue's Python consumer is far slower than the engine),
 BGX_BULK (1: one shared-memory message per harvest through
@@ -29,6 +33,22 @@ def _env_int(name, default):
     return int(os.environ.get(name, default))
 
 
+def gpus_for_worker(worker_id, n_gpu, n_workers=7, gpu_map=None):
+    """GPUs worker `worker_id` drives. gpu_map ("0;1;2;3;4;5;6,7": worker ids
+    separated by ';', GPUs by ','), else GPU g -> worker g mod n_workers, so
+    main.py's 7 workers (main.py:86) cover every GPU of an 8-GPU node."""
+    if gpu_map:
+        per = [p.strip() for p in gpu_map.split(";")]
+        if worker_id >= len(per) or not per[worker_id]:
+            return []
+        gpus = [int(x) for x in per[worker_id].split(",") if x.strip()]
+        bad = [g for g in gpus if not 0 <= g < n_gpu]
+        if bad:
+            raise ValueError(f"BGX_GPU_MAP names GPU(s) {bad}; {n_gpu} visible")
+        return gpus
+    return [g for g in range(n_gpu) if g % max(1, n_workers) == worker_id]
+
+
 class Worker:
     def __init__(self, worker_id, parameter_manager, experience_queue):
         self.worker_id = worker_id
@@ -38,49 +58,75 @@ class Worker:
         self.state_dict = self.parameter_manager.get_parameters()
         self.current_version = self.parameter_manager.get_version()
         n_gpu = torch.cuda.device_count()
-        self.device = worker_id if worker_id < n_gpu else None
+        self.devices = gpus_for_worker(worker_id, n_gpu, _env_int("BGX_WORKERS", 7), os.environ.get("BGX_GPU_MAP"))
+        self.device = self.devices[0] if self.devices else None
         self.lanes = _env_int("BGX_LANES", 4096)
+        self.balance = _env_int("BGX_BALANCE", 1) != 0
         self.ply = _env_int("BGX_PLY", 1)
         self.k_top = _env_int("BGX_K_TOP", 4)
         self.steps_per_harvest = _env_int("BGX_STEPS_PER_HARVEST", 100)
         self.max_pending = _env_int("BGX_MAX_PENDING", 2000)
-        self.engine = None
+        self.engines = []
+        self.engine = None   # the first GPU's engine
 
     def _ensure_engine(self):
-        if self.engine is None:
-            torch.cuda.set_device(self.device)
-            self.engine = Engine(lanes=self.lanes, seed=1000003 * (self.worker_id + 1), ply=self.ply,
-                                 k_top=self.k_top, lane_base=self.worker_id * self.lanes)
-            self.engine.set_weights(self.state_dict, self.temperature, self.current_version)
-        return self.engine
+        """One engine per GPU of this worker: global lanes [g * lanes, (g + 1) *
+        lanes) on GPU g, seeded per GPU (the lanes of GPU g are the same
+        whichever worker drives it)."""
+        if not self.engines:
+            for g in self.devices:
+                torch.cuda.set_device(g)
+                e = Engine(lanes=self.lanes, seed=1000003 * (g + 1), ply=self.ply, k_top=self.k_top,
+                           lane_base=g * self.lanes, balance=self.balance)
+                e.set_weights(self.state_dict, self.temperature, self.current_version)
+                self.engines.append(e)
+            torch.cuda.set_device(self.devices[0])
+            self.engine = self.engines[0]
+        return self.engines
 
     def _maybe_update(self):
         new_version = self.parameter_manager.get_version()
         if new_version > self.current_version:
             self.state_dict = self.parameter_manager.get_parameters()
             self.temperature = self.parameter_manager.get_temperature()
-            self.engine.set_weights(self.state_dict, self.temperature, new_version)
+            for e in self.engines:
+                e.set_weights(self.state_dict, self.temperature, new_version)
             self.current_version = new_version
+
+    def _step_all(self, steps):
+        engines = self._ensure_engine()
+        for e in engines:   # asynchronous: the GPUs step concurrently
+            with torch.cuda.device(e.device):
+                e.step(steps or self.steps_per_harvest)
+        harvests = []
+        for e in engines:
+            with torch.cuda.device(e.device):
+                harvests.append(e.harvest())
+        return harvests
 
     def play_episodes(self, steps=None):
         """Advance all lanes and return the Episodes that finished (already to_numpy()'d)."""
-        eng = self._ensure_engine()
-        eng.step(steps or self.steps_per_harvest)
-        return to_episodes(eng.harvest(), Episode, Experience, Player)
+        out = []
+        for h in self._step_all(steps):
+            out += to_episodes(h, Episode, Experience, Player)
+        return out
 
     def harvest_records(self, steps=None):
         """Advance all lanes; return the finished episodes as compact host arrays
-        (headers uint32 [n, 16], records uint32 [m, 12]) for the bulk queue path."""
-        eng = self._ensure_engine()
-        eng.step(steps or self.steps_per_harvest)
-        h = eng.harvest()
-        return (h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32))
+        (headers uint32 [n, 16], records uint32 [m, 12]) for the bulk queue path
+        (each episode's records contiguous, in header order, GPU by GPU)."""
+        hs = self._step_all(steps)
+        hdr = [h.headers.cpu().numpy().view(np.uint32) for h in hs]
+        rec = [h.records.cpu().numpy().view(np.uint32) for h in hs]
+        if len(hs) == 1:
+            return hdr[0], rec[0]
+        return np.concatenate(hdr), np.concatenate(rec)
 
     def run(self):
         if self.device is None:
             print(f"Worker {self.worker_id}: no GPU for this worker id; idle.")
             return
-        print(f"Worker {self.worker_id} starting on cuda:{self.device} with {self.lanes} lanes.")
+        print(f"Worker {self.worker_id} starting on cuda:{self.devices} with {self.lanes} lanes per GPU.")
         bulk = hasattr(self.experience_queue, "put_records") and os.environ.get("BGX_BULK", "1") != "0"
         while True:
             if bulk:

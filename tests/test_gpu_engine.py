@@ -393,3 +393,30 @@ def test_fused_greedy_and_ragged_lanes(weights_ckpt, fl, monkeypatch):
         runs.append(_by_episode(*_collect(e, 200, chunk=50)))
         e.close()
     _same_runs(*runs)
+
+
+@pytest.mark.parametrize("fl", ["16", "32"])
+def test_fused_balanced_launch_keeps_every_lane_game(weights_seed0, fl, monkeypatch):
+    """balance=True (include/bgx.h bgx_config.balance): step(n) runs n x lanes
+    lane-steps in total with the workgroups at their own pace. Every lane's
+    games are unchanged — each (lane, episode) both runs finished has identical
+    records — and the launch's lane-step total is the budget plus less than
+    one workgroup-step per workgroup."""
+    monkeypatch.setenv("BGX_FUSED_LANES", fl)
+    lanes, steps, chunk = 300, 200, 40
+    ref = _engine(weights_seed0, lanes=lanes, seed=23, ply=1, fused=True)
+    a = _by_episode(*_collect(ref, steps, chunk=chunk))
+    ref.close()
+    e = _engine(weights_seed0, lanes=lanes, seed=23, ply=1, fused=True, balance=True)
+    b = _by_episode(*_collect(e, steps, chunk=chunk))
+    st = e.stats()
+    e.close()
+    groups = (lanes + int(fl) - 1) // int(fl)
+    launches = steps // chunk
+    assert lanes * steps <= st["env_steps"] < lanes * steps + launches * groups * int(fl)
+    common = a.keys() & b.keys()
+    assert len(common) >= 0.8 * min(len(a), len(b)) and len(common) > 100
+    for key in common:
+        np.testing.assert_array_equal(a[key][0], b[key][0], err_msg=str(key))
+        for f in a[key][1]:
+            np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")

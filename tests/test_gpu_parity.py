@@ -202,3 +202,75 @@ def test_value_paths_within_tol(bgx_ops, which, weights_seed0, weights_ckpt):
     want = orc.value(w, x)
     got = net.value_boards(torch.from_numpy(boards).cuda(), torch.from_numpy(player).cuda()).cpu().numpy()
     assert np.max(np.abs(got - want)) < V_TOL
+
+
+def test_stateless_ops_reject_out_of_domain_inputs(bgx_ops, weights_seed0):
+    """The device check (include/bgx.h BGX_BADF_*) of every stateless entry
+    point: each rule rejects with BGX_E_ARG before any output is written, the
+    device flags equal the host rule's, and legal inputs pass."""
+    from bgx import BgxError
+    from test_abi import _host_check, domain_cases
+    cases = domain_cases()
+    boards = np.stack([c[1] for c in cases])
+    players = np.array([c[2] for c in cases], np.uint8)
+    dice = np.array([c[3] for c in cases], np.uint8)
+    # device flags == host flags, per case and for the whole batch
+    for k in range(len(cases)):
+        got = bgx_ops.check_boards(torch.from_numpy(boards[k:k + 1]).cuda(),
+                                   torch.from_numpy(players[k:k + 1]).cuda(),
+                                   torch.from_numpy(dice[k:k + 1]).cuda())
+        assert got == _host_check(boards[k:k + 1], players[k:k + 1], dice[k:k + 1]), cases[k][0]
+    assert bgx_ops.check_boards(torch.from_numpy(boards).cuda(), torch.from_numpy(players).cuda(),
+                                torch.from_numpy(dice).cuda()) == (31, 3)
+    net = bgx_ops.Net(weights_seed0)
+    for k, (name, b, p, d, want) in enumerate(cases):
+        bb = torch.from_numpy(np.stack([cases[0][1], b])).cuda()     # a legal row first
+        pp = torch.tensor([0, min(p, 255)], dtype=torch.uint8).cuda()
+        dd = torch.tensor([[3, 1], list(d)], dtype=torch.uint8).cuda()
+        for fn, bad in (
+                (lambda: bgx_ops.movegen(bb, pp, dd, cap=64), want),
+                (lambda: bgx_ops.encode(bb, pp), want & ~8),
+                (lambda: net.value_boards(bb, pp), want & ~8),
+                (lambda: net.two_ply(bb, pp), want & ~8)):
+            if bad:
+                with pytest.raises(BgxError, match="outside the board domain"):
+                    fn()
+            else:
+                fn()
+    torch.cuda.synchronize()
+
+
+def test_stateless_ops_thread_safe_scratch(bgx_ops):
+    """Concurrent bgx_movegen calls from several host threads on their own
+    streams (each call leases its own overflow counter / workspace) give the
+    single-threaded results."""
+    import threading
+    g = golden("movegen_cases.npz")
+    boards, player, dice = g["boards"][:400], g["player"][:400], g["dice"][:400]
+    want_out, want_cnt = _run_movegen(bgx_ops, boards, player, dice, 64)
+    errs, outs = [], {}
+
+    def work(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for rep in range(6):
+                    o, c = bgx_ops.movegen(torch.from_numpy(boards).cuda(), torch.from_numpy(player).cuda(),
+                                           torch.from_numpy(dice).cuda(), cap=64, stream=s)
+                    s.synchronize()
+                    outs[(t, rep)] = (o.cpu().numpy(), c.cpu().numpy())
+        except Exception as ex:   # noqa: BLE001
+            errs.append(ex)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs, errs
+    assert len(outs) == 24
+    for o, c in outs.values():
+        np.testing.assert_array_equal(c, want_cnt)
+        for i in range(len(c)):
+            k = min(int(c[i]), 64)
+            np.testing.assert_array_equal(o[i, :k], want_out[i, :k])

@@ -1,10 +1,13 @@
 """GPU engine vs the reference's own env trajectories, shard invariance and
 2-ply decisions against the oracle.
 
-* Replay: tests/golden/env_traj.npz holds 16 greedy
+* Replay: tests/golden/env_traj.npz holds greedy
   episodes that tools/gen_golden.py played with the reference's functions in
   the order BackgammonEnv.reset / step run them (backgammon_env.py:92-221,
-  worker.py:101-162), with every np.random.randint die recorded. The engine
+  worker.py:101-162), with every np.random.randint die recorded, under the
+  seed-0 weights and the shipped 2.1M checkpoint; they include close-outs,
+  primes, repeats of either after the reward was given, gammons, backgammons
+  and consecutive passes (test_oracle_golden.py counts them). The engine
   replays them with those dice scripted (bgx_engine_set_dice) and greedy
   play, and every decision must match: board before and after, mover through
   pass turns, dice, move count, action, V(s) / V(a) (1e-5), reward, done, win
@@ -57,10 +60,11 @@ def _episodes(e, steps, chunk=100):
     return out
 
 
+@pytest.mark.parametrize("wset", [0, 1])
 @pytest.mark.parametrize("fused", [False, True])
-def test_replay_reference_trajectories(weights_seed0, fused):
+def test_replay_reference_trajectories(weights_seed0, weights_ckpt, fused, wset):
     t = golden("env_traj.npz")
-    eps = t["episodes"]
+    eps = t["episodes"][t["weight_set"] == wset]
     n = len(eps)
     # after its episode a lane keeps playing (new games on 1-2 rolls): two
     # draws per env step for the rest of the 300 steps, plus the resets
@@ -68,7 +72,7 @@ def test_replay_reference_trajectories(weights_seed0, fused):
     dice = np.tile(np.array([1, 2], np.uint8), (n, width // 2 + 1))[:, :width].copy()
     for i, (d0, dn, _s0, _sn) in enumerate(eps):
         dice[i, :dn] = t["dice"][d0:d0 + dn]
-    e = _engine(weights_seed0, lanes=n, seed=0, ply=1, greedy=True, fused=fused)
+    e = _engine(weights_seed0 if wset == 0 else weights_ckpt, lanes=n, seed=0, ply=1, greedy=True, fused=fused)
     e.set_dice(dice)
     got = _episodes(e, 300, chunk=150)
     e.close()
@@ -105,7 +109,8 @@ def test_replay_reference_trajectories(weights_seed0, fused):
         if t["done"][last]:
             assert int(hdr[5]) & 0xFF == int(t["win_type"][last])
             assert (int(hdr[5]) >> 8) & 0xFF == int(t["player"][last])
-    assert checked == int((t["kind"] == 0).sum())
+    rows = np.concatenate([np.arange(s0, s0 + sn) for (_d0, _dn, s0, sn) in eps])
+    assert checked == int((t["kind"][rows] == 0).sum())
 
 
 def test_scripted_dice_need_greedy_and_report_exhaustion(weights_seed0):

@@ -84,3 +84,20 @@ def test_load_pth_round_trip(tmp_path):
     np.testing.assert_array_equal(w["b1"], sd["fc1.bias"].numpy())
     np.testing.assert_array_equal(w["w2"], sd["value_head.weight"].numpy().reshape(128))
     np.testing.assert_array_equal(w["b2"], sd["value_head.bias"].numpy())
+
+
+def test_seven_workers_cover_eight_gpus():
+    """main.py:86 starts exactly 7 workers; gpus_for_worker spreads a node's
+    GPUs over them (GPU g -> worker g mod 7: worker 0 drives GPUs 0 and 7),
+    or follows BGX_GPU_MAP."""
+    from multi.worker import gpus_for_worker
+    got = [gpus_for_worker(i, 8) for i in range(7)]
+    assert got == [[0, 7], [1], [2], [3], [4], [5], [6]]
+    assert sorted(g for gs in got for g in gs) == list(range(8))
+    assert [gpus_for_worker(i, 1) for i in range(7)] == [[0]] + [[]] * 6
+    m = "0;1;2;3;4;5;6,7"
+    assert [gpus_for_worker(i, 8, gpu_map=m) for i in range(7)] == [[0], [1], [2], [3], [4], [5], [6, 7]]
+    assert gpus_for_worker(3, 8, gpu_map="0;1") == []
+    import pytest
+    with pytest.raises(ValueError):
+        gpus_for_worker(0, 2, gpu_map="5")

@@ -1,7 +1,8 @@
 """Per-launch fixed cost of the fused 1-ply kernel: host wall time of one
 k-step launch (synchronised) for k in 1..300 at 8,192 lanes, fit t = F + k s.
 With BGX_FUSED_PROF=1 each engine also prints its last launch's per-workgroup
-durations at close. Development tool (tools/runs/r4d.sh)."""
+durations at close. BALANCE=1: balanced launches (bgx_config.balance).
+Development tool."""
 import os
 import sys
 import time
@@ -15,9 +16,10 @@ from bgx import Engine  # noqa: E402
 d = np.load(os.path.join(REPO, "tests", "golden", "weights_seed0.npz"))
 w = {k: d[k] for k in ("W1", "b1", "w2", "b2")}
 lanes = int(os.environ.get("LANES", "8192"))
+balance = os.environ.get("BALANCE", "0") == "1"
 res = []
 for k in (1, 2, 5, 20, 60, 300):
-    e = Engine(lanes=lanes, seed=3, ply=1)
+    e = Engine(lanes=lanes, seed=3, ply=1, balance=balance)
     e.set_weights(w, temperature=1.5, version=1)
     e.step(300)
     e.harvest()

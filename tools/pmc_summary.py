@@ -43,7 +43,7 @@ def main(out):
                      "tools/sq_counters.sh (sq_<leg>.json)",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts 1/2 of wide "
                          "coalesced reads; narrow movegen reads are uncalibrated, the raw value is kept beside it)"}
-    for leg in ("1ply_fused", "2ply_k4"):
+    for leg in ("1ply_fused", "2ply_k4", "2ply_kall"):
         f = per_kernel(os.path.join(out, f"pmc_{leg}_FETCH_SIZE"))
         w = per_kernel(os.path.join(out, f"pmc_{leg}_WRITE_SIZE"))
         if not f and not w:
@@ -76,7 +76,7 @@ def main(out):
                 legd[g]["steps_per_launch"] = FUSED_STEPS_PER_DISPATCH
                 legd[g]["hbm_bytes_per_step"] = legd[g]["hbm_bytes_per_launch"] / FUSED_STEPS_PER_DISPATCH
         # SQ counter ratios of the same leg's kernels (tools/sq_summary.py)
-        sq_leg = {"1ply_fused": "1ply", "2ply_k4": "2ply_k4"}[leg]
+        sq_leg = {"1ply_fused": "1ply", "2ply_k4": "2ply_k4", "2ply_kall": "2ply_kall"}[leg]
         try:
             sq = json.load(open(os.path.join(out, f"sq_{sq_leg}.json")))["kernels"]
             for g in ("movegen", "mlp", "fused"):
@@ -84,8 +84,9 @@ def main(out):
                     ks = [k for k in sq if group(k) == g and "movegen_pool" in k or (group(k) == g and g != "movegen")]
                     if ks:
                         k = ks[0]
-                        for r in ("valu_busy", "mfma_busy", "lds_busy", "wait_frac", "issue_stall_frac", "waves_per_cu"):
-                            if r in sq[k]:
+                        for r in ("valu_busy", "mfma_busy", "lds_busy", "salu_busy", "wait_frac", "issue_stall_frac",
+                                  "waves_per_cu"):
+                            if sq[k].get(r) is not None:
                                 legd[g][r] = sq[k][r]
                         legd[g]["sq_kernel"] = k
         except (OSError, ValueError, KeyError):

@@ -7,6 +7,8 @@ OUT=gpurun_out/${1:-sq}; LEG=${2:-2ply_k4}; RX=${3:-"movegen_pool|mlp_kernel_il"
 mkdir -p $OUT
 if [ $LEG = 2ply_k4 ]; then
   ARGS="--ply 2 --k-top 4 --steps 30 --warmup 10 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"
+elif [ $LEG = 2ply_kall ]; then
+  ARGS="--ply 2 --k-top 0 --steps 6 --warmup 2 --desync-steps 30 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"
 else
   ARGS="--steps 300 --warmup 100 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"
 fi

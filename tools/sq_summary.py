@@ -5,7 +5,8 @@
 GRBM_GUI_ACTIVE count cycles, GRBM_GUI_ACTIVE summed over the 8 XCDs):
   cycles        = GRBM_GUI_ACTIVE / 8 (the dispatch's GPU-busy cycles)
   valu_busy     = 4 * SQ_ACTIVE_INST_VALU / (cycles * 1024 SIMDs)
-  salu_busy     = 4 * SQ_ACTIVE_INST_SALU / (cycles * 256 CUs)   (one scalar unit per CU)
+  salu_busy     = 4 * SQ_ACTIVE_INST_SALU (or _SCA) / (cycles * 256 CUs)   (one scalar unit per CU;
+                  null when the counter is not collected)
   lds_busy      = 4 * SQ_ACTIVE_INST_LDS / (cycles * 256 CUs)
   mfma_busy     = SQ_VALU_MFMA_BUSY_CYCLES / (cycles * 1024 SIMDs)
   wait_frac     = SQ_WAIT_ANY / SQ_WAVE_CYCLES, issue_stall_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES,
@@ -35,19 +36,24 @@ def main(out, leg):
         per = {n: v / max(1, len(disp[k][n])) for n, v in c.items()}
         cyc = per.get("GRBM_GUI_ACTIVE", 0) / 8
         dv = {"dispatches": max(len(s) for s in disp[k].values()), "counters_per_dispatch": per}
+        # a ratio whose counter was not collected is null, never 0
+        def ratio(name, scale):
+            return scale * per[name] if name in per else None
         if cyc > 0:
             dv["cycles"] = cyc
-            dv["valu_busy"] = 4 * per.get("SQ_ACTIVE_INST_VALU", 0) / (cyc * 1024)
-            dv["salu_busy"] = 4 * per.get("SQ_ACTIVE_INST_SALU", 0) / (cyc * 256)
-            dv["lds_busy"] = 4 * per.get("SQ_ACTIVE_INST_LDS", 0) / (cyc * 256)
-            dv["mfma_busy"] = per.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (cyc * 1024)
-            dv["waves_per_cu"] = per.get("SQ_WAVE_CYCLES", 0) / (cyc / 4) / 256
+            dv["valu_busy"] = ratio("SQ_ACTIVE_INST_VALU", 4 / (cyc * 1024))
+            salu = next((n for n in ("SQ_ACTIVE_INST_SALU", "SQ_ACTIVE_INST_SCA") if n in per), None)
+            dv["salu_busy"] = ratio(salu, 4 / (cyc * 256)) if salu else None
+            dv["salu_counter"] = salu
+            dv["lds_busy"] = ratio("SQ_ACTIVE_INST_LDS", 4 / (cyc * 256))
+            dv["mfma_busy"] = ratio("SQ_VALU_MFMA_BUSY_CYCLES", 1 / (cyc * 1024))
+            dv["waves_per_cu"] = ratio("SQ_WAVE_CYCLES", 1 / (cyc / 4) / 256)
         wc = per.get("SQ_WAVE_CYCLES", 0)
         if wc:
-            dv["wait_frac"] = per.get("SQ_WAIT_ANY", 0) / wc
-            dv["issue_stall_frac"] = per.get("SQ_WAIT_INST_ANY", 0) / wc
-            dv["lds_issue_stall_frac"] = per.get("SQ_WAIT_INST_LDS", 0) / wc
-            dv["active_frac"] = per.get("SQ_ACTIVE_INST_ANY", 0) / wc
+            dv["wait_frac"] = ratio("SQ_WAIT_ANY", 1 / wc)
+            dv["issue_stall_frac"] = ratio("SQ_WAIT_INST_ANY", 1 / wc)
+            dv["lds_issue_stall_frac"] = ratio("SQ_WAIT_INST_LDS", 1 / wc)
+            dv["active_frac"] = ratio("SQ_ACTIVE_INST_ANY", 1 / wc)
         res["kernels"][k] = dv
     print(json.dumps(res, indent=1))
 
