@@ -100,6 +100,8 @@ class DeviceTrainer:
     def _hip_state(self):
         """Flat fp32 params / Adam moments (state_dict order) and the step count,
         taken over from the torch module / optimizer the first time."""
+        if self._flat is not None and self._flat.get("token") != self._module_token():
+            self._flat = None   # the module / optimizer changed outside the HIP updates: take it over again
         if self._flat is None:
             net, opt = self.policy_network, self.optimizer
             params = [dict(net.named_parameters())[k] for k in self._KEYS]
@@ -113,8 +115,20 @@ class DeviceTrainer:
                 v = torch.cat([x["exp_avg_sq"].reshape(-1) for x in st]).contiguous()
                 step = int(float(st[0]["step"]))
             self._flat = {"p": flat, "m": m, "v": v,
-                          "step": torch.tensor([step], dtype=torch.int32, device=self.device)}
+                          "step": torch.tensor([step], dtype=torch.int32, device=self.device),
+                          "token": self._module_token()}
         return self._flat
+
+    def _module_token(self):
+        """Identifies the module's parameters and the optimizer's moments as the
+        HIP backend last left them: every in-place write (load_state_dict,
+        copy_, an optimizer step) bumps a tensor's _version, and replacing the
+        optimizer state swaps the moment tensors."""
+        net, opt = self.policy_network, self.optimizer
+        params = [dict(net.named_parameters())[k] for k in self._KEYS]
+        st = [opt.state.get(p, {}) for p in params]
+        return (tuple(p._version for p in params),
+                tuple((id(x.get("exp_avg")), id(x.get("exp_avg_sq")), id(x.get("step"))) for x in st))
 
     def _sync_module(self):
         """Copy the HIP backend's weights / moments back into the torch module and
@@ -134,6 +148,7 @@ class DeviceTrainer:
                     st["exp_avg_sq"] = f["v"][o:o + n].view_as(p).clone()
                     st["step"] = torch.tensor(float(step))
                 o += n
+        f["token"] = self._module_token()
 
     def _update_hip(self, headers, records):
         from ._lib import check, lib, ptr, stream_handle
@@ -145,15 +160,21 @@ class DeviceTrainer:
         lens = hdr[:, 3].astype(np.int64)
         if len(lens) and int(lens.max()) > 2048:
             raise ValueError("bgx_td0_update: an episode has more than 2048 records")
+        if len(lens) and int(lens.min()) <= 0:
+            # the kernel skips an empty episode (no Adam step), while the metrics
+            # below divide by every episode: reject it instead of skewing them
+            raise ValueError("bgx_td0_update: an episode has no records")
         offs = torch.as_tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32), device=self.device)
         f = self._hip_state()
         metrics = torch.zeros(5, dtype=torch.float64, device=self.device)
         n_eps = len(lens)
         clip = float(self.grad_clip) if self.grad_clip is not None else 0.0
-        check(lib().bgx_td0_update(ptr(rec), ptr(offs), n_eps, ptr(f["p"]), ptr(f["m"]), ptr(f["v"]),
-                                   ptr(f["step"]), float(self.optimizer.param_groups[0]["lr"]),
-                                   float(self.gamma), clip, ptr(metrics), stream_handle(None)),
-              "bgx_td0_update")
+        with torch.cuda.device(self.device):   # the trainer's device and its current stream
+            check(lib().bgx_td0_update(ptr(rec), ptr(offs), n_eps, ptr(f["p"]), ptr(f["m"]), ptr(f["v"]),
+                                       ptr(f["step"]), float(self.optimizer.param_groups[0]["lr"]),
+                                       float(self.gamma), clip, ptr(metrics),
+                                       stream_handle(torch.cuda.current_stream(self.device))),
+                  "bgx_td0_update")
         self.total_episodes += n_eps
         self._sync_module()
         a = metrics.tolist()

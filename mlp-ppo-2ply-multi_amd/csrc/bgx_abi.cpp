@@ -452,6 +452,8 @@ int bgx_td0_update(const uint32_t* d_records, const int32_t* d_offs, int n_eps, 
         if (n_eps < 0 || (n_eps > 0 && (!d_records || !d_offs || !d_params || !d_adam_m || !d_adam_v || !d_step ||
                                         !d_metrics)))
             return fail(BGX_E_ARG, "bgx_td0_update: bad arguments (n_eps=%d)", n_eps);
+        DeviceScope ds(d_params);   // the kernel runs on the device holding the parameters
+        HIP_TRY(ds.err);
         bgx::TrainArgs a{};
         a.rec = d_records;
         a.offs = d_offs;

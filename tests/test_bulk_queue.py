@@ -144,3 +144,21 @@ def test_message_pack_round_trip():
     np.testing.assert_array_equal(r, r2)
     h0, r0 = unpack_message(pack_message(np.zeros((0, 16), np.uint32), np.zeros((0, 12), np.uint32)))
     assert h0.shape == (0, 16) and r0.shape == (0, 12)
+
+
+def test_queue_side_imports_without_torch():
+    """The CPU-side queue (multi.experience_queue, bgx.records) loads neither
+    torch nor libbgx.so: the package re-exports are lazy (PEP 562), while
+    `from multi import ParameterManager, Worker, ExperienceQueue,
+    worker_function` (main.py:2) still resolves."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    code = ("import sys; sys.path.insert(0, %r); import multi.experience_queue, bgx.records; "
+            "print('torch' in sys.modules, 'bgx._lib' in sys.modules)" % PKG)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout
+    assert out.split() == ["False", "False"]
+    code = ("import sys; sys.path.insert(0, %r); "
+            "from multi import ParameterManager, Worker, ExperienceQueue, worker_function; print('ok')" % PKG)
+    assert subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                          check=True).stdout.strip() == "ok"

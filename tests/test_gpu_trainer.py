@@ -129,3 +129,39 @@ def test_hip_trainer_matches_torch_and_reference(weights_seed0):
     tt.update_records(hdr[:40], rec[:n0])
     for k in sd0:
         torch.testing.assert_close(pm_h.sd[k], pm_t.sd[k], rtol=3e-4, atol=6e-5)
+
+
+def test_hip_trainer_takes_outside_module_changes(weights_seed0):
+    """A load_state_dict on the module between two HIP updates is not
+    overwritten by the backend's flat copy (the next update starts from the
+    loaded weights, as the torch backend does), and an episode with no
+    records is rejected instead of skewing the metrics."""
+    from bgx import Engine
+    from bgx.net import BackgammonPolicyNetwork
+    from bgx.trainer import DeviceTrainer
+    eng = Engine(lanes=512, seed=13)
+    eng.set_weights(weights_seed0, 1.5, 1)
+    eng.step(300)
+    h = eng.harvest()
+    eng.close()
+    hdr = h.headers[:20].cpu()
+    n = int(hdr[:, 3].sum())
+    rec = h.records[:n]
+    torch.manual_seed(2)
+    sd0 = BackgammonPolicyNetwork().state_dict()
+    torch.manual_seed(3)
+    sd1 = BackgammonPolicyNetwork().state_dict()
+    pm_h, pm_t = _PM(sd0), _PM(sd1)
+    th = DeviceTrainer(pm_h, device="cuda", batch_episode_size=20, backend="hip")
+    tt = DeviceTrainer(pm_t, device="cuda", batch_episode_size=20, backend="hip")
+    th.update_records(hdr, rec)
+    th.policy_network.load_state_dict(sd1)          # an outside write (e.g. a checkpoint restore)
+    th.optimizer.state.clear()
+    th.update_records(hdr, rec)
+    tt.update_records(hdr, rec)                     # a fresh trainer from sd1
+    for k in sd0:
+        torch.testing.assert_close(pm_h.sd[k], pm_t.sd[k], rtol=0, atol=0)
+    bad = hdr.clone()
+    bad[0, 3] = 0
+    with pytest.raises(ValueError, match="no records"):
+        th.update_records(bad, rec)

@@ -88,6 +88,83 @@ def test_env_greedy_trajectories():
             assert bool(r.prime_reward) == bool(t["prime"][s])
             if t["kind"][s] == 0:
                 np.testing.assert_array_equal(env.board, t["after"][s])
+                if not t["done"][s]:
+                    mover = int(t["player"][s])
+                    assert orc.predicate("is_closed_out", env.board, mover) == bool(t["closed_pred"][s])
+                    assert orc.predicate("made_at_least_five_prime", env.board, mover) == bool(t["prime_pred"][s])
+
+
+def _env_events(t):
+    """Event counts of env_traj.npz (tools/gen_golden.py episode_events)."""
+    k, rew = t["kind"], t["reward"]
+    prev_pass = np.concatenate([[False], k[:-1] == 1])
+    first = np.zeros(len(k), bool)
+    first[t["episodes"][:, 2]] = True
+    return dict(close_out=int(t["close_out"].sum()), prime=int(t["prime"].sum()),
+                close_repeat=int((t["closed_pred"] & ~t["close_out"]).sum()),
+                prime_repeat=int((t["prime_pred"] & ~t["prime"]).sum()),
+                backgammon=int((t["win_type"] == 3).sum()), gammon=int((t["win_type"] == 2).sum()),
+                pass_run=int(((k == 1) & prev_pass & ~first).sum()),
+                shaping_rewards=sorted(set(rew[(rew > 0) & (rew < 1)].tolist())))
+
+
+def test_env_fixture_covers_shaping_and_terminal_events():
+    """The reference-generated trajectories hold every reward path of
+    backgammon_env.py:167-213: close-outs (+0.30) and primes (+0.20), either
+    predicate holding again after the player's reward was given (no second
+    reward: once per player per game), gammons, backgammons, consecutive
+    passes; under both weight sets (the seed-0 net and the 2.1M checkpoint)."""
+    t = golden("env_traj.npz")
+    ev = _env_events(t)
+    assert ev["close_out"] >= 10 and ev["prime"] >= 10, ev
+    assert ev["close_repeat"] >= 1 and ev["prime_repeat"] >= 1, ev
+    assert ev["backgammon"] >= 3 and ev["gammon"] >= 3 and ev["pass_run"] >= 1, ev
+    # the rewards are torch fp32 (backgammon_env.py:165-213): 0.2f and 0.3f exactly
+    assert ev["shaping_rewards"] == [float(np.float32(0.2)), float(np.float32(0.3))], ev
+    assert set(np.unique(t["weight_set"]).tolist()) == {0, 1}
+    # the once-per-player rule: at most one close-out and one prime reward per player per game
+    for (d0, dn, s0, sn) in t["episodes"]:
+        rows = slice(s0, s0 + sn)
+        for pl in (0, 1):
+            mine = t["player"][rows] == pl
+            assert t["close_out"][rows][mine].sum() <= 1 and t["prime"][rows][mine].sum() <= 1
+
+
+def test_close_out_and_prime_never_coincide():
+    """A step cannot earn both shaping rewards (0.30 + 0.20): a close-out needs
+    the mover's six home points made (12 checkers), and a counted 5-prime needs
+    an opponent checker past the prime's end (env_helper.py:167-242), i.e. on
+    one of those home points, or 10 more checkers for a prime outside home.
+    Checked exhaustively over the predicate fixture's boards and 20,000 random
+    closed-out boards on the oracle."""
+    p = golden("predicates.npz")
+    assert not np.any(p["closed_out"] & p["prime"])
+    rng = np.random.default_rng(5)
+    n = 0
+    for _ in range(20000):
+        b = np.zeros(52, np.uint8)
+        mover = int(rng.integers(2))
+        home = np.arange(18, 24) if mover == 0 else np.arange(0, 6)
+        b[24 * mover + home] = 2
+        rest = 3
+        while rest:
+            i = int(rng.integers(24))
+            if i in home or b[24 * (1 - mover) + i] == 0:
+                k = int(rng.integers(1, rest + 1))
+                b[24 * mover + i] += k
+                rest -= k
+        b[48 + (1 - mover)] = int(rng.integers(1, 4))
+        left = 15 - b[48 + (1 - mover)]
+        free = [i for i in range(24) if b[24 * mover + i] == 0]
+        for i in rng.choice(free, size=min(len(free), 6), replace=False):
+            k = int(min(left, rng.integers(1, 4)))
+            b[24 * (1 - mover) + i] += k
+            left -= k
+        b[50 + (1 - mover)] = left
+        if orc.predicate("is_closed_out", b, mover):
+            n += 1
+            assert not orc.predicate("made_at_least_five_prime", b, mover), b
+    assert n == 20000
 
 
 def test_two_ply_exact_mode(weights_seed0, weights_ckpt):
