@@ -5,8 +5,9 @@
 GRBM_GUI_ACTIVE count cycles, GRBM_GUI_ACTIVE summed over the 8 XCDs):
   cycles        = GRBM_GUI_ACTIVE / 8 (the dispatch's GPU-busy cycles)
   valu_busy     = 4 * SQ_ACTIVE_INST_VALU / (cycles * 1024 SIMDs)
-  salu_busy     = 4 * SQ_ACTIVE_INST_SALU (or _SCA) / (cycles * 256 CUs)   (one scalar unit per CU;
-                  null when the counter is not collected)
+  salu_busy     = SQ_INST_CYCLES_SALU / (cycles * 256 CUs)   (rocprofv3's SALUBusy expression; one
+                  scalar unit per CU; null when the counter is not collected)
+  sca_active_per_cu = 4 * SQ_ACTIVE_INST_SCA / (cycles * 256 CUs)   (waves' SALU + SMEM issue cycles per CU)
   lds_busy      = 4 * SQ_ACTIVE_INST_LDS / (cycles * 256 CUs)
   mfma_busy     = SQ_VALU_MFMA_BUSY_CYCLES / (cycles * 1024 SIMDs)
   wait_frac     = SQ_WAIT_ANY / SQ_WAVE_CYCLES, issue_stall_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES,
@@ -42,9 +43,10 @@ def main(out, leg):
         if cyc > 0:
             dv["cycles"] = cyc
             dv["valu_busy"] = ratio("SQ_ACTIVE_INST_VALU", 4 / (cyc * 1024))
-            salu = next((n for n in ("SQ_ACTIVE_INST_SALU", "SQ_ACTIVE_INST_SCA") if n in per), None)
-            dv["salu_busy"] = ratio(salu, 4 / (cyc * 256)) if salu else None
-            dv["salu_counter"] = salu
+            # rocprofv3's own SALUBusy: SQ_INST_CYCLES_SALU / CU_NUM / GRBM_GUI_ACTIVE (per XCD);
+            # SQ_ACTIVE_INST_SCA (quad-cycles of SALU + SMEM per wave) beside it
+            dv["salu_busy"] = ratio("SQ_INST_CYCLES_SALU", 1 / (cyc * 256))
+            dv["sca_active_per_cu"] = ratio("SQ_ACTIVE_INST_SCA", 4 / (cyc * 256))
             dv["lds_busy"] = ratio("SQ_ACTIVE_INST_LDS", 4 / (cyc * 256))
             dv["mfma_busy"] = ratio("SQ_VALU_MFMA_BUSY_CYCLES", 1 / (cyc * 1024))
             dv["waves_per_cu"] = ratio("SQ_WAVE_CYCLES", 1 / (cyc / 4) / 256)
