@@ -125,29 +125,62 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
                  fused=not args.no_fused, balance=not args.no_balance)
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
+    hg = None
+    if world > 1 and args.gather == "host":
+        from bgx import hostgather
+        hg = hostgather.setup(rank, world, hostgather.slot_bytes_for(lanes, args.harvest_every), dst=0,
+                              device=torch.cuda.current_device())
+    seq = [0]
 
     def run(n):
-        # the gather of a harvest stays in flight while the next steps run and
-        # is waited at the next harvest (or the end of the run)
-        left, pending = n, None
+        # The harvest is queued behind each launch (harvest_enqueue) and the next
+        # launch is queued before the host looks at it, so the device never waits
+        # for the host; chunk i's episodes are handed on (gathered at N > 1) while
+        # chunk i + 1 runs, and that hand-off is complete before the harvest
+        # buffers it reads are reused (two harvests later).
+        left, pending_t, inflight = n, None, None
 
-        def collect(p):
-            eps, recs = p.wait()
-            if rank == 0:
-                gathered[0] += eps
-                gathered[1] += recs
+        def consume(t):
+            nonlocal inflight
+            h = eng.harvest_fetch(t)
+            if world == 1:
+                return
+            if hg is not None:      # DMA engines into host shared memory; no collective
+                seq[0] += 1
+                if rank == 0:
+                    for part in hg.collect(seq[0], copy=False):
+                        if part is not None:
+                            gathered[0] += part[0].shape[0]
+                            gathered[1] += part[1].shape[0]
+                    gathered[0] += h.n_episodes
+                    gathered[1] += h.n_records
+                    hg.ack(seq[0])
+                else:
+                    inflight = hg.publish(h)
+            else:                   # RCCL point-to-point to rank 0
+                inflight = bdist.gather_episodes(h, dst=0, async_op=True)
+
+        def settle():
+            nonlocal inflight
+            if inflight is not None:
+                r = inflight.wait()
+                if hg is None and rank == 0:
+                    gathered[0] += r[0]
+                    gathered[1] += r[1]
+                inflight = None
 
         while left > 0:
             k = min(harvest_every, left)
+            settle()               # the previous hand-off, before its buffers can be reused
             eng.step(k)
-            h = eng.harvest()
-            if world > 1:
-                if pending is not None:
-                    collect(pending)
-                pending = bdist.gather_episodes(h, dst=0, async_op=True)
+            t = eng.harvest_enqueue()
+            if pending_t is not None:
+                consume(pending_t)
+            pending_t = t
             left -= k
-        if pending is not None:
-            collect(pending)
+        if pending_t is not None:
+            consume(pending_t)
+        settle()
 
     # lanes start together from the reset; `desync` untimed steps
     # (harvested, and gathered at N > 1, like the timed ones) spread them over
@@ -179,6 +212,10 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
         d_tm["elapsed_s"] = el_tm
         d_tm["lanes"] = lanes
     eng.close()
+    if hg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+        hg.close()
     return el, d, tm, d_tm, gathered
 
 
@@ -388,6 +425,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true",
                     help="1-ply: one launch per phase and step instead of the fused persistent step kernel")
+    ap.add_argument("--gather", choices=("host", "rccl"), default="host",
+                    help="N > 1 episode gather to rank 0: 'host' = DMA-engine copies into host shared memory "
+                         "(no kernels, no collective per harvest); 'rccl' = RCCL point-to-point over xGMI")
     ap.add_argument("--no-balance", action="store_true",
                     help="fused 1-ply: every lane runs exactly the steps of a call (lockstep) instead of the "
                          "balanced launch (a step(n) call = n x lanes lane-steps, faster workgroups run ahead)")
@@ -470,8 +510,10 @@ def main():
                        "harvest_every": args.harvest_every,
                        "engine": ("fused step kernel" + ("" if args.no_balance else ", balanced launches")
                                   if args.ply == 1 and not args.no_fused else "phased launches"),
-                       "parallelism": (f"lanes sharded x{world}, RCCL episode gather to rank 0 "
-                                       f"({BACKEND})" if world > 1 else "single GPU")},
+                       "parallelism": ((f"lanes sharded x{world}, episode gather to rank 0 over the DMA engines "
+                                        f"into host shared memory" if args.gather == "host" else
+                                        f"lanes sharded x{world}, RCCL episode gather to rank 0 ({BACKEND})")
+                                       if world > 1 else "single GPU")},
             "desync_steps": head["desync_steps"],
             "world_size": world, "env_steps_per_rank": head["env_steps_per_rank"],
             "decisions_per_s": head["decisions_per_s"], "episodes_per_s": head["episodes_per_s"],

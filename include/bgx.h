@@ -180,7 +180,7 @@ int bgx_sync(bgx_engine* e);
 
 /* Finished episodes since the last harvest (Episode/Experience,
  * environments/episode.py:5-84). Both arrays are DEVICE memory owned by the
- * engine, valid until the next bgx_harvest/bgx_step; each episode's records
+ * engine, valid until the second bgx_harvest after this one; each episode's records
  * are contiguous, in header order:
  *   headers [n_episodes][16] u32: global lane, episode no., first record,
  *     n_records, env steps, win_type | winner << 8 | flags << 16, the final
@@ -204,6 +204,16 @@ typedef struct bgx_harvest_info {
     const uint32_t* d_records;
 } bgx_harvest_info;
 int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream);
+
+/* bgx_harvest in two halves, so the host does not stall the device between
+ * steps: bgx_harvest_enqueue queues the harvest on `stream` (behind the
+ * engine's last step; the next bgx_step waits for it) and returns a ticket at
+ * once; bgx_harvest_fetch(ticket) waits for that harvest and fills `out` as
+ * bgx_harvest does. Two buffers alternate: a ticket's arrays stay valid until
+ * the second bgx_harvest_enqueue after it, and only the last two tickets can
+ * be fetched. (bgx_harvest = enqueue + fetch.) */
+int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream);
+int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out);
 
 typedef struct bgx_stats {
     uint64_t env_steps;     /* lane steps (passes included) */
@@ -236,6 +246,17 @@ int bgx_get_timing(bgx_engine* e, double* ms_movegen, int* n_movegen, double* ms
 int bgx_td0_update(const uint32_t* d_records, const int32_t* d_offs, int n_eps, float* d_params,
                    float* d_adam_m, float* d_adam_v, int* d_step, float lr, float gamma, float grad_clip,
                    double* d_metrics, void* stream);
+
+/* Copy-engine transfer helpers (bgx/hostgather.py: the episode gather of
+ * the ranks of one node through host shared memory, replacing the pickled
+ * queue of src/main.py:115-133 / multi/experience_queue.py:5-13 without
+ * using compute units): page-lock an existing host range (a shared-memory
+ * segment) for DMA, and an asynchronous copy between any two of device /
+ * page-locked host memory on `stream` (hipMemcpyAsync, hipMemcpyDefault:
+ * DMA engines, no kernel). */
+int bgx_host_register(void* h_ptr, uint64_t bytes);
+int bgx_host_unregister(void* h_ptr);
+int bgx_copy_async(void* dst, const void* src, uint64_t bytes, void* stream);
 
 /* Convert between u8[52] boards and the engine's packed boards (device). */
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream);

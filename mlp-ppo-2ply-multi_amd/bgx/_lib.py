@@ -72,12 +72,17 @@ SIGNATURES = {
     "bgx_step": (c_int, [c_void_p, c_int, c_void_p]),
     "bgx_sync": (c_int, [c_void_p]),
     "bgx_harvest": (c_int, [c_void_p, ctypes.POINTER(HarvestInfo), c_void_p]),
+    "bgx_harvest_enqueue": (c_int, [c_void_p, ctypes.POINTER(c_int), c_void_p]),
+    "bgx_harvest_fetch": (c_int, [c_void_p, c_int, ctypes.POINTER(HarvestInfo)]),
     "bgx_get_stats": (c_int, [c_void_p, ctypes.POINTER(Stats)]),
     "bgx_set_timing": (c_int, [c_void_p, c_int]),
     "bgx_get_timing": (c_int, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int),
                                ctypes.POINTER(c_double), ctypes.POINTER(c_int)]),
     "bgx_td0_update": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                c_float, c_float, c_void_p, c_void_p]),
+    "bgx_host_register": (c_int, [c_void_p, c_u64]),
+    "bgx_host_unregister": (c_int, [c_void_p]),
+    "bgx_copy_async": (c_int, [c_void_p, c_void_p, c_u64, c_void_p]),
     "bgx_pack": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "bgx_unpack": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
 }

@@ -104,6 +104,25 @@ class Engine:
     def harvest(self, stream=None, clone=True) -> Harvest:
         info = HarvestInfo()
         check(lib().bgx_harvest(self._h, ctypes.byref(info), stream_handle(stream)), "bgx_harvest")
+        return self._harvest_from(info, clone)
+
+    def harvest_enqueue(self, stream=None) -> int:
+        """Queue a harvest behind the last step and return its ticket at once
+        (bgx_harvest_enqueue): the next step() can be launched before the host
+        looks at the result."""
+        t = ctypes.c_int(0)
+        check(lib().bgx_harvest_enqueue(self._h, ctypes.byref(t), stream_handle(stream)), "bgx_harvest_enqueue")
+        return int(t.value)
+
+    def harvest_fetch(self, ticket: int, clone=False) -> Harvest:
+        """Wait for a queued harvest (one of the last two tickets). Without
+        clone the tensors alias the engine's buffers, valid until the second
+        harvest_enqueue after `ticket`."""
+        info = HarvestInfo()
+        check(lib().bgx_harvest_fetch(self._h, int(ticket), ctypes.byref(info)), "bgx_harvest_fetch")
+        return self._harvest_from(info, clone)
+
+    def _harvest_from(self, info, clone):
         if info.n_episodes == 0:   # nothing finished: shared empty tensors, no allocation
             if self._empty is None:
                 self._empty = Harvest(torch.zeros((0, EP_WORDS), dtype=torch.int32, device=self.device),

@@ -1,0 +1,215 @@
+"""Episode gather of the ranks of one node over the DMA engines (no kernels,
+no collective per harvest).
+
+The reference hands finished episodes from its 7 workers to main.py through a
+pickled multiprocessing.Queue (src/main.py:115-133,
+src/multi/experience_queue.py:5-13): a host-side hand-off. Here every rank
+runs its own Engine on its GPU; after a harvest it copies the compact
+headers (64 B) and records (48 B) device -> host straight into a
+shared-memory segment that is page-locked for DMA (bgx_host_register), with
+hipMemcpyAsync on a side stream (bgx_copy_async: the copy engines, so the
+transfer runs while the persistent fused kernel holds every compute unit).
+The counts travel in the same segment: there is no per-harvest collective.
+The trainer rank reads every peer's batch from host memory (where main.py's
+consumer wants them) and acknowledges it.
+
+Protocol (per rank r != dst, batch numbers 1, 2, ... ; two slots):
+  publish(h): wait until dst acknowledged batch seq - 2 (the slot's previous
+              batch), enqueue the two copies into slot seq % 2, return a
+              Pending; Pending.wait() waits for the copies, then stores the
+              counts and finally the batch number (the store that publishes).
+  collect(seq) on dst: for every peer, wait until its published number
+              reaches seq, read counts and data, store the acknowledgement.
+A rank can run at most one batch ahead of dst's reads; nothing else couples
+the ranks. Segment header (i64): [0] published batch, [1 + 2 s] episodes and
+[2 + 2 s] records of the batch in slot s, [5] acknowledged batch (written by
+dst). The counts are per slot: a rank one batch ahead rewrites only its
+other slot's.
+"""
+from __future__ import annotations
+
+import os
+import secrets
+import time
+from multiprocessing import shared_memory
+
+import numpy as np
+import torch
+
+from .records import EP_WORDS, REC_WORDS
+
+HDR = 64
+EP_BYTES, REC_BYTES = EP_WORDS * 4, REC_WORDS * 4
+
+
+def slot_bytes_for(lanes: int, steps_per_harvest: int, max_steps: int = 300) -> int:
+    """A harvest holds at most one record per lane-step since the last one,
+    plus the not yet harvested part of every lane's current episode, and at
+    most one header per 13 lane-steps (the shortest game) + one per lane."""
+    recs = lanes * (steps_per_harvest + max_steps)
+    eps = lanes * (steps_per_harvest // 13 + 2)
+    return ((recs * REC_BYTES + eps * EP_BYTES) + 4095) & ~4095
+
+
+class Pending:
+    def __init__(self, gather, seq, n_eps, n_recs, slot, event):
+        self.g, self.seq, self.n_eps, self.n_recs, self.slot, self.event = gather, seq, n_eps, n_recs, slot, event
+
+    def wait(self):
+        if self.event is not None:
+            self.event.synchronize()
+        c = self.g.ctrl[self.g.rank]
+        c[1 + 2 * self.slot], c[2 + 2 * self.slot] = self.n_eps, self.n_recs
+        c[0] = self.seq            # publishes (aligned 8-byte store after the counts)
+        return self.seq
+
+
+class HostGather:
+    """One per rank. `tag` names the segments (every rank must pass the same
+    one, e.g. from make_tag()); slot_bytes from slot_bytes_for()."""
+
+    def __init__(self, rank: int, world: int, tag: str, slot_bytes: int, dst: int = 0, device=None,
+                 timeout: float = 120.0):
+        self.rank, self.world, self.dst, self.tag = rank, world, dst, tag
+        self.slot_bytes = int(slot_bytes)
+        self.timeout = timeout
+        self.device = device
+        self.seq = 0
+        self._mine = shared_memory.SharedMemory(name=self._name(rank), create=True,
+                                                size=HDR + 2 * self.slot_bytes)
+        self.shm = {rank: self._mine}
+        np.ndarray((8,), np.int64, buffer=self._mine.buf[:HDR])[:] = 0
+        self.ctrl = {rank: np.ndarray((8,), np.int64, buffer=self._mine.buf[:HDR])}
+        self._registered = None
+        self._stream = None
+        if device is not None and torch.cuda.is_available():
+            from ._lib import check, lib
+            addr = np.frombuffer(self._mine.buf, np.uint8).ctypes.data
+            check(lib().bgx_host_register(addr, HDR + 2 * self.slot_bytes), "bgx_host_register")
+            self._registered = addr
+            self._stream = torch.cuda.Stream(device=device)
+
+    def _name(self, r):
+        return f"bgx_hg_{self.tag}_{r}"
+
+    def attach(self):
+        """dst: open every peer's segment (after all ranks constructed theirs)."""
+        if self.rank != self.dst:
+            return
+        for r in range(self.world):
+            if r not in self.shm:
+                s = shared_memory.SharedMemory(name=self._name(r))
+                self.shm[r] = s
+                self.ctrl[r] = np.ndarray((8,), np.int64, buffer=s.buf[:HDR])
+
+    def _slot(self, r, slot):
+        base = HDR + slot * self.slot_bytes
+        return self.shm[r].buf[base:base + self.slot_bytes]
+
+    def _spin(self, cond, what):
+        t0 = time.monotonic()
+        while not cond():
+            if time.monotonic() - t0 > self.timeout:
+                raise TimeoutError(f"HostGather rank {self.rank}: {what}")
+            time.sleep(0.0002)
+
+    def publish(self, h) -> Pending:
+        """Rank != dst: start the copy of a Harvest into this rank's segment."""
+        self.seq += 1
+        seq, slot = self.seq, self.seq % 2
+        c = self.ctrl[self.rank]
+        self._spin(lambda: int(c[5]) >= seq - 2, f"dst did not read batch {seq - 2}")
+        n_eps, n_recs = h.n_episodes, h.n_records
+        need = n_eps * EP_BYTES + n_recs * REC_BYTES
+        if need > self.slot_bytes:
+            raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")
+        dst = np.frombuffer(self._slot(self.rank, slot), np.uint8)
+        if n_eps == 0:
+            return Pending(self, seq, 0, 0, slot, None)
+        if h.headers.is_cuda and self._stream is not None:
+            from ._lib import check, lib
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(h.headers.device))
+            self._stream.wait_event(ev)
+            base = dst.ctypes.data
+            s = self._stream.cuda_stream
+            check(lib().bgx_copy_async(base, h.headers.data_ptr(), n_eps * EP_BYTES, s), "bgx_copy_async")
+            check(lib().bgx_copy_async(base + n_eps * EP_BYTES, h.records.data_ptr(), n_recs * REC_BYTES, s),
+                  "bgx_copy_async")
+            done = torch.cuda.Event()
+            done.record(self._stream)
+            # the engine's buffers must outlive the copy: the caller waits this
+            # Pending before its next harvest (bgx_harvest reuses them)
+            return Pending(self, seq, n_eps, n_recs, slot, done)
+        hb = h.headers.cpu().numpy().view(np.uint8).reshape(-1)
+        rb = h.records.cpu().numpy().view(np.uint8).reshape(-1)
+        dst[:hb.size] = hb
+        dst[hb.size:hb.size + rb.size] = rb
+        return Pending(self, seq, n_eps, n_recs, slot, None)
+
+    def collect(self, seq: int, copy: bool = True):
+        """dst: every peer's batch `seq` as (headers uint32 [n, 16], records
+        uint32 [m, 12]) host arrays, in rank order (dst's own entry is None:
+        the caller has its harvest). copy=False returns views that stay valid
+        until the peer reuses the slot (two batches later)."""
+        out = []
+        for r in range(self.world):
+            if r == self.dst:
+                out.append(None)
+                continue
+            c = self.ctrl[r]
+            self._spin(lambda: int(c[0]) >= seq, f"rank {r} did not publish batch {seq}")
+            slot = seq % 2
+            n_eps, n_recs = int(c[1 + 2 * slot]), int(c[2 + 2 * slot])
+            raw = np.frombuffer(self._slot(r, slot), np.uint8)
+            hdr = raw[:n_eps * EP_BYTES].view(np.uint32).reshape(-1, EP_WORDS)
+            rec = raw[n_eps * EP_BYTES:n_eps * EP_BYTES + n_recs * REC_BYTES].view(np.uint32).reshape(-1, REC_WORDS)
+            if copy:
+                hdr, rec = hdr.copy(), rec.copy()
+            out.append((hdr, rec))
+            if copy:
+                c[5] = seq      # acknowledged: the peer may reuse this slot
+        return out
+
+    def ack(self, seq: int):
+        """dst, after collect(seq, copy=False): release every peer's slot."""
+        for r in range(self.world):
+            if r != self.dst:
+                self.ctrl[r][5] = seq
+
+    def close(self):
+        if self._registered is not None:
+            from ._lib import lib
+            lib().bgx_host_unregister(self._registered)
+            self._registered = None
+        for r, s in list(self.shm.items()):
+            try:
+                if r != self.rank:
+                    s.close()
+            except (BufferError, OSError):
+                pass
+        self.ctrl = {}
+        try:
+            self._mine.close()
+            self._mine.unlink()
+        except (BufferError, FileNotFoundError, OSError):
+            pass
+        self.shm = {}
+
+
+def make_tag() -> str:
+    """A fresh segment tag (rank 0 makes it; broadcast it to the others)."""
+    return f"{os.getpid()}_{secrets.token_hex(4)}"
+
+
+def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None) -> HostGather:
+    """Collective once (torch.distributed): agree on a tag, create the
+    segments, let dst attach them. No collective afterwards."""
+    import torch.distributed as dist
+    obj = [make_tag() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    g = HostGather(rank, world, obj[0], slot_bytes, dst=dst, device=device)
+    dist.barrier()
+    g.attach()
+    dist.barrier()
+    return g

@@ -137,7 +137,7 @@ struct bgx_engine {
     int32_t* cand_off = nullptr;
     int32_t* cand_cnt = nullptr;
     unsigned* ctr = nullptr;   // [3] ep, [4] err; per-step (zeroed each step): [8] flat, [9] reply, [10] ovf, [11] ovf2;
-                               // [12..13] balanced-launch lane-step counter
+                               // [12..15] balanced-launch counters (lane-steps, finished workgroups)
     unsigned long long* stats = nullptr;
     int32_t* sel = nullptr;
     uint32_t* sel_rows = nullptr;
@@ -158,12 +158,17 @@ struct bgx_engine {
     int fcap = 0;
     unsigned long long* fprof = nullptr;   // BGX_FUSED_PROF: phase clocks, printed at destroy
     // harvest: records of at most L x ring (every unharvested record of every lane)
-    uint32_t* out_records = nullptr;
-    int32_t* d_offs = nullptr;     // [ep_cap + 1]
-    uint32_t* d_info = nullptr;    // [4] harvest_scan_kernel totals
-    uint32_t* h_info = nullptr;    // host-mapped copy, written by harvest_scan_kernel itself
+    // two harvest buffers (bgx_harvest_enqueue / _fetch): ticket t uses slot t & 1
+    uint32_t* out_records[2] = {nullptr, nullptr};
+    uint32_t* out_headers[2] = {nullptr, nullptr};   // [ep_cap][16] copies of the finished episodes' headers
+    int32_t* d_offs[2] = {nullptr, nullptr};     // [ep_cap + 1]
+    uint32_t* d_info[2] = {nullptr, nullptr};    // [4] harvest_scan_kernel totals
+    uint32_t* h_info = nullptr;    // [2][4] host-mapped copies, written by harvest_scan_kernel itself
     uint32_t* h_info_dev = nullptr;   // its device address
-    hipEvent_t hev = nullptr;
+    hipEvent_t hev = nullptr;         // the engine's last step, for a harvest on another stream
+    hipEvent_t hdone[2] = {nullptr, nullptr};   // a slot's harvest kernels finished
+    hipStream_t hstream = nullptr;    // stream of the last enqueued harvest (the next step waits for it)
+    int h_tickets = 0;                // harvests enqueued so far
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;   // pairs: movegen, mlp
@@ -185,7 +190,7 @@ struct bgx_engine {
 
 namespace {
 constexpr int C_EP = 3, C_ERR = 4, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
-constexpr int C_BUDGET = 12;   // [12..13]: the balanced fused launch's lane-step counter (u64)
+constexpr int C_BUDGET = 12;   // [12..15]: the balanced fused launch's lane-step and finished-workgroup counters (u64)
 }
 
 static int flag_error(unsigned f) {
@@ -471,6 +476,31 @@ int bgx_td0_update(const uint32_t* d_records, const int32_t* d_offs, int n_eps, 
     });
 }
 
+int bgx_host_register(void* h_ptr, uint64_t bytes) {
+    return guarded("bgx_host_register", [&]() -> int {
+        if (!h_ptr || bytes == 0) return fail(BGX_E_ARG, "bgx_host_register: bad arguments");
+        HIP_TRY(hipHostRegister(h_ptr, (size_t)bytes, hipHostRegisterPortable));
+        return BGX_OK;
+    });
+}
+
+int bgx_host_unregister(void* h_ptr) {
+    return guarded("bgx_host_unregister", [&]() -> int {
+        if (!h_ptr) return fail(BGX_E_ARG, "bgx_host_unregister: null pointer");
+        HIP_TRY(hipHostUnregister(h_ptr));
+        return BGX_OK;
+    });
+}
+
+int bgx_copy_async(void* dst, const void* src, uint64_t bytes, void* stream) {
+    return guarded("bgx_copy_async", [&]() -> int {
+        if (bytes == 0) return BGX_OK;
+        if (!dst || !src) return fail(BGX_E_ARG, "bgx_copy_async: null pointer");
+        HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, (hipStream_t)stream));
+        return BGX_OK;
+    });
+}
+
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream) {
     return guarded("bgx_pack", [&]() -> int {
         if (n < 0) return fail(BGX_E_ARG, "bgx_pack: n=%d", n);
@@ -739,13 +769,16 @@ int bgx_engine_destroy(bgx_engine* e) {
             hipFree(e->fprof);
         }
         void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
-                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records,
-                      e->d_offs, e->d_info, e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
+                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records[0],
+                      e->out_records[1], e->out_headers[0], e->out_headers[1], e->d_offs[0], e->d_offs[1],
+                      e->d_info[0], e->d_info[1], e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
                       e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->dice_tab};
         for (void* p : ps) hipFree(p);
         for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
         if (e->gexec) hipGraphExecDestroy(e->gexec);
         if (e->hev) hipEventDestroy(e->hev);
+        for (hipEvent_t ev : e->hdone)
+            if (ev) hipEventDestroy(ev);
         if (e->h_info) hipHostFree(e->h_info);
         if (e->cap) hipStreamDestroy(e->cap);
         bgx_net_destroy(e->net);
@@ -815,10 +848,15 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         ALLOC(d.harv, L);
         ALLOC(d.ring, (size_t)L * ring * bgx::REC_WORDS);
         ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
-        ALLOC(e->out_records, (size_t)L * ring * bgx::REC_WORDS);
-        ALLOC(e->d_offs, (size_t)ep_cap + 1);
-        ALLOC(e->d_info, 4);
-        if (!rc && (hipHostMalloc((void**)&e->h_info, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+        for (int b = 0; b < 2; ++b) {
+            ALLOC(e->out_records[b], (size_t)L * ring * bgx::REC_WORDS);
+            ALLOC(e->out_headers[b], (size_t)ep_cap * bgx::EP_WORDS);
+            ALLOC(e->d_offs[b], (size_t)ep_cap + 1);
+            ALLOC(e->d_info[b], 4);
+            if (!rc && hipEventCreateWithFlags(&e->hdone[b], hipEventDisableTiming) != hipSuccess)
+                rc = fail(BGX_E_HIP, "hipEventCreate failed");
+        }
+        if (!rc && (hipHostMalloc((void**)&e->h_info, 8 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
                         hipSuccess ||
                     hipHostGetDevicePointer((void**)&e->h_info_dev, e->h_info, 0) != hipSuccess))
             rc = fail(BGX_E_HIP, "hipHostMalloc (mapped) failed");
@@ -1114,6 +1152,10 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
                         e->cfg.ring - e->cfg.max_steps);
         HIP_TRY(hipSetDevice(e->device));
         hipStream_t s = (hipStream_t)stream;
+        // an enqueued harvest on another stream reads the rings and resets the
+        // episode list: the step waits for it (an event, no host wait)
+        if (e->h_tickets > 0 && e->hstream != s)
+            HIP_TRY(hipStreamWaitEvent(s, e->hdone[(e->h_tickets - 1) & 1], 0));
         e->last = s;
         if (n_steps == 0) return BGX_OK;
         // timed runs launch directly (events between the kernels); otherwise the
@@ -1155,9 +1197,9 @@ int bgx_sync(bgx_engine* e) {
     });
 }
 
-int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
-    return guarded("bgx_harvest", [&]() -> int {
-        if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest: null pointer");
+int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream) {
+    return guarded("bgx_harvest_enqueue", [&]() -> int {
+        if (!e || !ticket) return fail(BGX_E_ARG, "bgx_harvest_enqueue: null pointer");
         HIP_TRY(hipSetDevice(e->device));
         hipStream_t s = (hipStream_t)stream;
         // order after the engine's last step (another stream): an event, no host wait
@@ -1166,25 +1208,50 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
             HIP_TRY(hipEventRecord(e->hev, e->last));
             HIP_TRY(hipStreamWaitEvent(s, e->hev, 0));
         }
+        const int t = e->h_tickets, b = t & 1;
         // offsets and totals on the device (harvest_scan_kernel, which also writes
-        // {episodes, records, error flags} straight into host-mapped memory), then
-        // the record gather only when there is an episode to gather
-        HIP_TRY(bgx_launch_harvest_scan(&e->d, e->d_offs, e->d_info, e->h_info_dev, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (e->h_info[0] > 0 && !e->h_info[2]) {
-            HIP_TRY(bgx_launch_harvest_gather(&e->d, e->d_offs, e->d_info, e->out_records, s));
-            HIP_TRY(hipStreamSynchronize(s));
-        }
-        const uint32_t flags = e->h_info[2];
+        // {episodes, records, error flags} into host-mapped memory), then the copy
+        // of the finished episodes' headers and records (a persistent grid that
+        // reads the episode count on the device: no host round trip in between)
+        HIP_TRY(bgx_launch_harvest_scan(&e->d, e->d_offs[b], e->d_info[b], e->h_info_dev + 4 * b, s));
+        HIP_TRY(bgx_launch_harvest_gather(&e->d, e->d_offs[b], e->d_info[b], e->out_headers[b], e->out_records[b],
+                                          s));
+        HIP_TRY(hipEventRecord(e->hdone[b], s));
+        e->hstream = s;
+        e->h_tickets = t + 1;
+        *ticket = t;
+        return BGX_OK;
+    });
+}
+
+int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out) {
+    return guarded("bgx_harvest_fetch", [&]() -> int {
+        if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest_fetch: null pointer");
+        if (ticket < 0 || ticket >= e->h_tickets || ticket < e->h_tickets - 2)
+            return fail(BGX_E_ARG, "bgx_harvest_fetch: ticket %d is not one of the last two harvests (%d enqueued)",
+                        ticket, e->h_tickets);
+        HIP_TRY(hipSetDevice(e->device));
+        const int b = ticket & 1;
+        HIP_TRY(hipEventSynchronize(e->hdone[b]));
+        const uint32_t* info = e->h_info + 4 * b;
+        const uint32_t flags = info[2];
         if (flags) {
             HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
             return flag_error(flags);
         }
-        out->n_episodes = (int)e->h_info[0];
-        out->n_records = (int)e->h_info[1];
-        out->d_headers = e->d.ep_list;
-        out->d_records = e->out_records;
+        out->n_episodes = (int)info[0];
+        out->n_records = (int)info[1];
+        out->d_headers = e->out_headers[b];
+        out->d_records = e->out_records[b];
         return BGX_OK;
+    });
+}
+
+int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream) {
+    return guarded("bgx_harvest", [&]() -> int {
+        int t = 0;
+        if (int rc = bgx_harvest_enqueue(e, &t, stream)) return rc;
+        return bgx_harvest_fetch(e, t, out);
     });
 }
 

@@ -326,11 +326,15 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
 // count comes from harvest_scan_kernel)
 __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
                                                      const int32_t* __restrict__ offs,
-                                                     const uint32_t* __restrict__ info, uint32_t* __restrict__ out) {
+                                                     const uint32_t* __restrict__ info, uint32_t* __restrict__ hout,
+                                                     uint32_t* __restrict__ out) {
     const int n_eps = (int)info[0];
     constexpr int Q = REC_WORDS / 4;
     for (int ep = blockIdx.x; ep < n_eps; ep += gridDim.x) {
         const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
+        // the header too: the episode list is refilled by the next step
+        if (threadIdx.x < EP_WORDS / 4)
+            ((uint4*)(hout + (size_t)ep * EP_WORDS))[threadIdx.x] = ((const uint4*)h)[threadIdx.x];
         const int lane = (int)h[0] - e.lane_base;
         const uint32_t first = h[2], nrec = h[3];
         const uint4* src = (const uint4*)(e.ring + (size_t)lane * e.R * REC_WORDS);
@@ -383,7 +387,8 @@ extern "C" hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* 
 }
 
 extern "C" hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
-                                                uint32_t* out, hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::gather_kernel, dim3(1024), dim3(256), 0, stream, *e, e->ep_list, offsets, info, out);
+                                                uint32_t* hout, uint32_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::gather_kernel, dim3(1024), dim3(256), 0, stream, *e, e->ep_list, offsets, info, hout,
+                       out);
     return hipGetLastError();
 }

@@ -144,8 +144,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         const int na = nlive < NA ? nlive : NA, nbl = nlive - na;   // lanes stepped before / in the last round
         // step s runs iff ticket(s): lockstep, s < n_steps; balanced, s < n_cap and
         // the launch's lane-step total before this workgroup-step is below the
-        // budget (thread 0 takes step s + 1's ticket while step s runs; the barrier
-        // after tier 1 publishes it)
+        // budget (thread 0 takes step s + 1's ticket late in step s, before the
+        // MLP phase's last barrier, which publishes it: a workgroup commits to a
+        // further step as late as the choice phase allows, so the launch's tail
+        // after the budget runs out is about one step)
         auto ticket = [&](int s) -> int {
             if (f.budget <= 0) return s < f.n_steps;
             if (s >= f.n_cap) return 0;
@@ -156,7 +158,6 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         __syncthreads();
         const int n_iter = f.budget > 0 ? f.n_cap : f.n_steps;
         for (int step = 0; step < n_iter && T.go[step & 1]; ++step) {
-            if (t == 0) T.go[(step + 1) & 1] = ticket(step + 1);
             n_steps += (unsigned long long)nlive;
             // ---- 1. tier-1 movegen of the wave's lanes in its slice
             if (prof && t == 0) tc = wall_clock64();
@@ -362,6 +363,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             // ---- 3. the first batch's rows into the scratch
             const int n_tiles = (nr + 31) >> 5;
             stage(0, n_tiles < FT ? n_tiles : FT);
+            if (n_tiles == 0 && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // no MLP batch this step
             __syncthreads();
             tick(2);
             // ---- 4. value MLP: (32-board tile, m-tile) items over the waves,
@@ -407,6 +409,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                         else f.vbuf[(size_t)(g * FL + v) * (f.cap + 1) + k] = val;
                     }
                 }
+                if (tb + FT >= n_tiles && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // the last batch
                 __syncthreads();
                 if (tb + FT < n_tiles) {
                     stage(tb + FT, n_tiles - tb - FT < FT ? n_tiles - tb - FT : FT);
@@ -510,6 +513,15 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         atomicAdd(e.stats + 3, n_rows);
         atomicAdd(e.stats + 4, n_steps);
         atomicAdd(e.stats + 5, n_fb);
+        if (f.budget > 0) {
+            // the last workgroup to finish zeroes the lane-step counter for the
+            // next launch (stream order: no memset launch in between)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (atomicAdd(f.budget_ctr + 1, 1ull) == (unsigned long long)gridDim.x - 1ull) {
+                __hip_atomic_store(f.budget_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(f.budget_ctr + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 
@@ -560,10 +572,6 @@ extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t s
     // balanced only when every workgroup owns one lane group (a workgroup that
     // walks several groups would spend the budget on its first ones)
     if (a.budget > 0 && (groups > blocks || !a.budget_ctr || a.n_cap < a.n_steps)) a.budget = 0;
-    if (a.budget > 0) {
-        const hipError_t e = hipMemsetAsync(a.budget_ctr, 0, sizeof(unsigned long long), stream);
-        if (e != hipSuccess) return e;
-    }
     if (fl == 32) {
         if (a.prof)
             hipLaunchKernelGGL((bgx::fused_step_kernel<true, 32>), g, b, bgx::FCfg<32>::LDS, stream, a);

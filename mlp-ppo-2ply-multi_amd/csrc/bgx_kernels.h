@@ -149,10 +149,11 @@ struct FusedArgs {
     int lanes_per_wg;            // 16 or 32 game lanes per workgroup; 0: the launcher picks (32 when
                                  //   every CU still gets a workgroup)
     // balanced launch (bgx_config.balance): each workgroup-step takes a ticket of
-    // its lanes from *budget_ctr (zeroed per launch) and steps while the running
-    // total is below `budget` lane-steps, at most n_cap steps; budget <= 0: every
-    // lane runs exactly n_steps (lockstep). The launcher balances only when each
-    // workgroup owns one lane group.
+    // its lanes from budget_ctr[0] and steps while the running total is below
+    // `budget` lane-steps, at most n_cap steps; budget <= 0: every lane runs
+    // exactly n_steps (lockstep). budget_ctr[1] counts finished workgroups; the
+    // last one zeroes both (budget_ctr is zero at engine create). The launcher
+    // balances only when each workgroup owns one lane group.
     long long budget;
     int n_cap;
     unsigned long long* budget_ctr;
@@ -198,9 +199,10 @@ hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t
 hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out, hipStream_t stream);
 hipError_t bgx_launch_td0(const bgx::TrainArgs* args, hipStream_t stream);
 // harvest: episode offsets / totals (info[4] on the device, hinfo[4] host-mapped
-// or null), then the records gather (launched only when there is an episode)
+// or null), then the headers + records gather (persistent grid; the episode
+// count is read on the device)
 hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* hinfo,
                                    hipStream_t stream);
 hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
-                                     uint32_t* out, hipStream_t stream);
+                                     uint32_t* hout, uint32_t* out, hipStream_t stream);
 }

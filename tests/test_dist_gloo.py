@@ -120,3 +120,58 @@ def test_gloo_world2_distributed_parameter_manager():
         assert ver == 4 and abs(temp - (1.5 - 1.0 * 3 / 4000)) < 1e-12   # parameter_manager.py:101-111
         assert calls == [(0.5, 1.5, 1), (3.0, temp, 4)]  # engine re-armed once per propagated version
         assert b1 == 3.0 and w2shape == (1, 128)
+
+
+def _hg_worker(rank, world, port, out):
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    import torch.distributed as dist
+    from bgx import hostgather
+    from bgx.engine import Harvest
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = hostgather.setup(rank, world, slot_bytes=1 << 16, dst=0)
+    got = []
+    for seq in range(1, 6):
+        # rank r's batch seq: (r + seq) % 3 episodes (some empty), 2 records each
+        ne = (rank + seq) % 3
+        hdr = torch.full((ne, 16), 1000 * rank + seq, dtype=torch.int32)
+        rec = torch.arange(2 * ne * 12, dtype=torch.int32).view(-1, 12) + 100 * seq
+        if rank == 0:
+            parts = g.collect(seq)
+            got.append([None if p is None else (p[0].copy(), p[1].copy()) for p in parts])
+        else:
+            g.publish(Harvest(hdr, rec)).wait()
+    if rank == 0:
+        out.put(got)
+    dist.barrier()
+    g.close()
+    dist.destroy_process_group()
+
+
+def test_gloo_world3_host_gather():
+    """bgx.hostgather: ranks hand their harvests to rank 0 through host shared
+    memory (the DMA-engine path of bench.py --gather host; here CPU tensors),
+    double-buffered, empty batches included, exact bytes, no collective per
+    batch (ranks 1 and 2 may run a batch ahead of rank 0's reads)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hg_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == 5
+    for seq, parts in enumerate(got, start=1):
+        assert parts[0] is None
+        for r in (1, 2):
+            hdr, rec = parts[r]
+            ne = (r + seq) % 3
+            assert hdr.shape == (ne, 16) and rec.shape == (2 * ne, 12)
+            assert np.all(hdr == 1000 * r + seq)
+            np.testing.assert_array_equal(rec.reshape(-1), np.arange(2 * ne * 12) + 100 * seq)

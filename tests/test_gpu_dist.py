@@ -93,3 +93,79 @@ def test_gloo_world2_gathers_real_harvests(weights_seed0):
             np.testing.assert_array_equal(merged[key][1], ref[key][1], err_msg=str(key))
         total += len(ref)
     assert total > 100
+
+
+def _hg_rank(rank, world, port, L, steps, out):
+    import sys
+    from conftest import PKG, golden
+    sys.path.insert(0, PKG)
+    import torch
+    import torch.distributed as dist
+    from bgx import Engine, hostgather
+    from bgx import dist as bdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = hostgather.setup(rank, world, hostgather.slot_bytes_for(L, steps), dst=0, device=0)
+    w = {k: golden("weights_seed0.npz")[k] for k in ("W1", "b1", "w2", "b2")}
+    base, n = bdist.lane_block(rank, L)
+    e = Engine(lanes=n, lane_base=base, seed=17)
+    e.set_weights(w, 1.5, 1)
+    got, pend = [], None
+    for seq, chunk in enumerate((steps // 2, steps - steps // 2), start=1):
+        e.step(chunk)
+        h = e.harvest()
+        if rank == 0:
+            parts = g.collect(seq)
+            parts[0] = (h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32))
+            got.append(parts)
+        else:
+            g.publish(h).wait()      # DMA-engine copy into the shared segment, then publish
+    e.close()
+    if rank == 0:
+        out.put(got)
+    dist.barrier()
+    g.close()
+    dist.destroy_process_group()
+
+
+def test_host_gather_world2_real_harvests(weights_seed0):
+    """bench.py --gather host with real engines: two ranks on cuda:0, rank 1's
+    harvests reach rank 0 through page-locked shared memory by the copy
+    engines (bgx_copy_async); merged == one Engine over both lane blocks."""
+    from bgx import Engine
+    from bgx.records import episode_bounds
+    L, steps = 128, 240
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hg_rank, args=(r, 2, port, L, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    e = Engine(lanes=2 * L, seed=17)
+    e.set_weights(weights_seed0, 1.5, 1)
+    want = []
+    for chunk in (steps // 2, steps - steps // 2):
+        e.step(chunk)
+        h = e.harvest()
+        want.append((h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32)))
+    e.close()
+
+    def by_episode(hdr, rec):
+        offs, _ = episode_bounds(hdr)
+        return {(int(r[0]), int(r[1])): (r.copy(), rec[offs[i]:offs[i + 1]]) for i, r in enumerate(hdr)}
+
+    for parts, (wh, wr) in zip(got, want):
+        merged = {}
+        for hh, rr in parts:
+            merged.update(by_episode(hh, rr))
+        ref = by_episode(wh, wr)
+        assert merged.keys() == ref.keys() and len(ref) > 20
+        for key in ref:
+            np.testing.assert_array_equal(merged[key][0], ref[key][0], err_msg=str(key))
+            np.testing.assert_array_equal(merged[key][1], ref[key][1], err_msg=str(key))

@@ -420,3 +420,34 @@ def test_fused_balanced_launch_keeps_every_lane_game(weights_seed0, fl, monkeypa
         np.testing.assert_array_equal(a[key][0], b[key][0], err_msg=str(key))
         for f in a[key][1]:
             np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_pipelined_harvest_equals_synchronous(weights_seed0, fused):
+    """harvest_enqueue / harvest_fetch (the next step queued before the host
+    reads a harvest; two alternating buffers) deliver exactly the episodes of
+    the synchronous harvest(); a stale ticket is refused."""
+    from bgx import BgxError
+    a = _engine(weights_seed0, lanes=96, seed=29, ply=1, fused=fused)
+    want = _by_episode(*_collect(a, 200, chunk=40))
+    a.close()
+    from bgx.episodes import decode_records
+    b = _engine(weights_seed0, lanes=96, seed=29, ply=1, fused=fused)
+    hdrs, recs, pend = [], [], None
+    for _ in range(5):
+        b.step(40)
+        t = b.harvest_enqueue()
+        if pend is not None:
+            h = b.harvest_fetch(pend)
+            hdr = h.headers.cpu().numpy().view(np.uint32)
+            hdrs.append(hdr)
+            recs.append(decode_records(hdr, h.records))
+        pend = t
+    h = b.harvest_fetch(pend)
+    hdr = h.headers.cpu().numpy().view(np.uint32)
+    hdrs.append(hdr)
+    recs.append(decode_records(hdr, h.records))
+    with pytest.raises(BgxError, match="ticket"):
+        b.harvest_fetch(pend - 2)
+    b.close()
+    _same_runs(want, _by_episode(hdrs, recs))
