@@ -156,7 +156,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
                     gathered[1] += h.n_records
                     hg.ack(seq[0])
                 else:
-                    inflight = hg.publish(h)
+                    inflight = hg.publish(h, ready=True)   # harvest_fetch waited for the arrays
             else:                   # RCCL point-to-point to rank 0
                 inflight = bdist.gather_episodes(h, dst=0, async_op=True)
 

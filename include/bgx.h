@@ -256,7 +256,21 @@ int bgx_td0_update(const uint32_t* d_records, const int32_t* d_offs, int n_eps, 
  * DMA engines, no kernel). */
 int bgx_host_register(void* h_ptr, uint64_t bytes);
 int bgx_host_unregister(void* h_ptr);
-int bgx_copy_async(void* dst, const void* src, uint64_t bytes, void* stream);
+int bgx_copy_async(void* dst, const void* src, uint64_t bytes, int kind, void* stream);   /* kind: 0 default
+                                  (inferred), 1 host->device, 2 device->host, 3 device->device, 4 device->device
+                                  on the DMA engines (hipMemcpyDeviceToDeviceNoCU; also into page-locked host
+                                  memory, which the device addresses directly) */
+
+/* Device -> host copy on a DMA engine (SDMA, through the HSA runtime; the
+ * HIP runtime here serves such copies with blit kernels, which need compute
+ * units and queue behind a persistent kernel). h_dst must lie in a range
+ * page-locked with bgx_host_register; the copy starts at once (the caller has
+ * made d_src ready, e.g. by bgx_harvest_fetch) and *ticket identifies it;
+ * bgx_dma_wait(ticket, timeout_ms <= 0: no limit) waits for it and releases the
+ * ticket (exactly once per ticket). BGX_E_STATE when the device has no DMA
+ * engine for the direction. */
+int bgx_dma_copy_d2h(void* h_dst, const void* d_src, uint64_t bytes, int device, uint64_t* ticket);
+int bgx_dma_wait(uint64_t ticket, int timeout_ms);
 
 /* Convert between u8[52] boards and the engine's packed boards (device). */
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream);

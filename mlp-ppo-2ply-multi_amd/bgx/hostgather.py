@@ -6,9 +6,11 @@ pickled multiprocessing.Queue (src/main.py:115-133,
 src/multi/experience_queue.py:5-13): a host-side hand-off. Here every rank
 runs its own Engine on its GPU; after a harvest it copies the compact
 headers (64 B) and records (48 B) device -> host straight into a
-shared-memory segment that is page-locked for DMA (bgx_host_register), with
-hipMemcpyAsync on a side stream (bgx_copy_async: the copy engines, so the
-transfer runs while the persistent fused kernel holds every compute unit).
+shared-memory segment that is page-locked for DMA (bgx_host_register), on a
+DMA engine (bgx_dma_copy_d2h: SDMA through the HSA runtime, so the transfer
+runs while the persistent fused kernel holds every compute unit; the HIP
+runtime here would serve hipMemcpyAsync with a blit kernel, which waits for
+free compute units — BGX_HG_COPY=hip selects that path).
 The counts travel in the same segment: there is no per-harvest collective.
 The trainer rank reads every peer's batch from host memory (where main.py's
 consumer wants them) and acknowledges it.
@@ -40,6 +42,7 @@ from .records import EP_WORDS, REC_WORDS
 
 HDR = 64
 EP_BYTES, REC_BYTES = EP_WORDS * 4, REC_WORDS * 4
+COPY_KIND = int(os.environ.get("BGX_HG_COPY_KIND", "2"))   # bgx_copy_async kind: 2 = device -> host
 
 
 def slot_bytes_for(lanes: int, steps_per_harvest: int, max_steps: int = 300) -> int:
@@ -52,12 +55,18 @@ def slot_bytes_for(lanes: int, steps_per_harvest: int, max_steps: int = 300) -> 
 
 
 class Pending:
-    def __init__(self, gather, seq, n_eps, n_recs, slot, event):
+    def __init__(self, gather, seq, n_eps, n_recs, slot, event, dma=()):
         self.g, self.seq, self.n_eps, self.n_recs, self.slot, self.event = gather, seq, n_eps, n_recs, slot, event
+        self.dma = dma
 
     def wait(self):
         if self.event is not None:
             self.event.synchronize()
+        if self.dma:
+            from ._lib import check, lib
+            for t in self.dma:
+                check(lib().bgx_dma_wait(t, int(self.g.timeout * 1000)), "bgx_dma_wait")
+            self.dma = ()
         c = self.g.ctrl[self.g.rank]
         c[1 + 2 * self.slot], c[2 + 2 * self.slot] = self.n_eps, self.n_recs
         c[0] = self.seq            # publishes (aligned 8-byte store after the counts)
@@ -82,6 +91,9 @@ class HostGather:
         self.ctrl = {rank: np.ndarray((8,), np.int64, buffer=self._mine.buf[:HDR])}
         self._registered = None
         self._stream = None
+        # device -> host path: "dma" (bgx_dma_copy_d2h, SDMA engine) or "hip"
+        # (hipMemcpyAsync on a side stream: a blit kernel on this ROCm)
+        self.copy = os.environ.get("BGX_HG_COPY", "dma")
         if device is not None and torch.cuda.is_available():
             from ._lib import check, lib
             addr = np.frombuffer(self._mine.buf, np.uint8).ctypes.data
@@ -113,8 +125,10 @@ class HostGather:
                 raise TimeoutError(f"HostGather rank {self.rank}: {what}")
             time.sleep(0.0002)
 
-    def publish(self, h) -> Pending:
-        """Rank != dst: start the copy of a Harvest into this rank's segment."""
+    def publish(self, h, ready: bool = False) -> Pending:
+        """Rank != dst: start the copy of a Harvest into this rank's segment.
+        ready=True: the harvest's device arrays are complete (bgx_harvest_fetch
+        waited for them); otherwise the current stream is synchronized first."""
         self.seq += 1
         seq, slot = self.seq, self.seq % 2
         c = self.ctrl[self.rank]
@@ -126,6 +140,20 @@ class HostGather:
         dst = np.frombuffer(self._slot(self.rank, slot), np.uint8)
         if n_eps == 0:
             return Pending(self, seq, 0, 0, slot, None)
+        if h.headers.is_cuda and self._stream is not None and self.copy == "dma":
+            # DMA engine (bgx_dma_copy_d2h): the copy runs beside a persistent kernel
+            import ctypes
+            from ._lib import check, lib
+            if not ready:
+                torch.cuda.current_stream(h.headers.device).synchronize()
+            base = dst.ctypes.data
+            t1, t2 = ctypes.c_uint64(0), ctypes.c_uint64(0)
+            dev = h.headers.device.index
+            check(lib().bgx_dma_copy_d2h(base, h.headers.data_ptr(), n_eps * EP_BYTES, dev, ctypes.byref(t1)),
+                  "bgx_dma_copy_d2h")
+            check(lib().bgx_dma_copy_d2h(base + n_eps * EP_BYTES, h.records.data_ptr(), n_recs * REC_BYTES, dev,
+                                         ctypes.byref(t2)), "bgx_dma_copy_d2h")
+            return Pending(self, seq, n_eps, n_recs, slot, None, dma=(t1.value, t2.value))
         if h.headers.is_cuda and self._stream is not None:
             from ._lib import check, lib
             ev = torch.cuda.Event()
@@ -133,9 +161,10 @@ class HostGather:
             self._stream.wait_event(ev)
             base = dst.ctypes.data
             s = self._stream.cuda_stream
-            check(lib().bgx_copy_async(base, h.headers.data_ptr(), n_eps * EP_BYTES, s), "bgx_copy_async")
-            check(lib().bgx_copy_async(base + n_eps * EP_BYTES, h.records.data_ptr(), n_recs * REC_BYTES, s),
+            check(lib().bgx_copy_async(base, h.headers.data_ptr(), n_eps * EP_BYTES, COPY_KIND, s),
                   "bgx_copy_async")
+            check(lib().bgx_copy_async(base + n_eps * EP_BYTES, h.records.data_ptr(), n_recs * REC_BYTES, COPY_KIND,
+                                       s), "bgx_copy_async")
             done = torch.cuda.Event()
             done.record(self._stream)
             # the engine's buffers must outlive the copy: the caller waits this

@@ -4,6 +4,8 @@
 // per-step launch sequence and error reporting. All game logic runs in the
 // HIP kernels (bgx_movegen.hip, bgx_mlp.hip, bgx_encode.hip, bgx_engine.hip).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -356,6 +358,72 @@ int require_domain(const char* what, Scratch* sc, const uint8_t* boards, const u
 
 }  // namespace
 
+// ---- DMA-engine copies (SDMA through the HSA runtime). On this ROCm the HIP
+// runtime serves device <-> host hipMemcpyAsync with blit kernels, which need
+// compute units and so queue behind a persistent kernel; these copies go to a
+// DMA engine explicitly (hsa_amd_memory_async_copy_on_engine, forced SDMA).
+namespace {
+struct DmaDev {
+    bool ready = false;
+    hsa_agent_t gpu{}, cpu{};
+    hsa_amd_sdma_engine_id_t engine = HSA_AMD_SDMA_ENGINE_0;
+};
+std::mutex g_dma_mu;
+DmaDev g_dma[64];
+
+struct AgentQuery {
+    uint32_t bdf = 0, domain = 0;
+    hsa_agent_t gpu{}, cpu{};
+    bool have_gpu = false, have_cpu = false;
+};
+
+hsa_status_t find_agents(hsa_agent_t a, void* data) {
+    AgentQuery* q = (AgentQuery*)data;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && !q->have_cpu) {
+        q->cpu = a;
+        q->have_cpu = true;
+    } else if (t == HSA_DEVICE_TYPE_GPU && !q->have_gpu) {
+        uint32_t bdf = 0, dom = 0;
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+        if (bdf == q->bdf && dom == q->domain) {
+            q->gpu = a;
+            q->have_gpu = true;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+int dma_setup(int dev, DmaDev** out) {
+    std::lock_guard<std::mutex> g(g_dma_mu);
+    if (dev < 0 || dev >= 64) return fail(BGX_E_ARG, "bgx_dma: device %d", dev);
+    DmaDev& d = g_dma[dev];
+    if (!d.ready) {
+        int bus = 0, slot = 0, dom = 0;
+        HIP_TRY(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev));
+        HIP_TRY(hipDeviceGetAttribute(&slot, hipDeviceAttributePciDeviceId, dev));
+        HIP_TRY(hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dev));
+        if (hsa_init() != HSA_STATUS_SUCCESS) return fail(BGX_E_STATE, "bgx_dma: hsa_init failed");
+        AgentQuery q;
+        q.bdf = ((uint32_t)bus << 8) | ((uint32_t)slot << 3);
+        q.domain = (uint32_t)dom;
+        hsa_iterate_agents(find_agents, &q);
+        if (!q.have_gpu || !q.have_cpu) return fail(BGX_E_STATE, "bgx_dma: no HSA agent for device %d", dev);
+        uint32_t mask = 0;
+        if (hsa_amd_memory_copy_engine_status(q.cpu, q.gpu, &mask) != HSA_STATUS_SUCCESS || mask == 0)
+            return fail(BGX_E_STATE, "bgx_dma: no DMA engine available for device %d -> host", dev);
+        d.gpu = q.gpu;
+        d.cpu = q.cpu;
+        d.engine = (hsa_amd_sdma_engine_id_t)(mask & (~mask + 1u));   // the lowest available engine
+        d.ready = true;
+    }
+    *out = &d;
+    return BGX_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int bgx_abi_version(void) { return BGX_ABI_VERSION; }
@@ -492,11 +560,50 @@ int bgx_host_unregister(void* h_ptr) {
     });
 }
 
-int bgx_copy_async(void* dst, const void* src, uint64_t bytes, void* stream) {
+int bgx_copy_async(void* dst, const void* src, uint64_t bytes, int kind, void* stream) {
     return guarded("bgx_copy_async", [&]() -> int {
         if (bytes == 0) return BGX_OK;
-        if (!dst || !src) return fail(BGX_E_ARG, "bgx_copy_async: null pointer");
-        HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, (hipStream_t)stream));
+        if (!dst || !src || kind < 0 || kind > 4) return fail(BGX_E_ARG, "bgx_copy_async: bad arguments");
+        const hipMemcpyKind k[5] = {hipMemcpyDefault, hipMemcpyHostToDevice, hipMemcpyDeviceToHost,
+                                    hipMemcpyDeviceToDevice, hipMemcpyDeviceToDeviceNoCU};
+        HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, k[kind], (hipStream_t)stream));
+        return BGX_OK;
+    });
+}
+
+int bgx_dma_copy_d2h(void* h_dst, const void* d_src, uint64_t bytes, int device, uint64_t* ticket) {
+    return guarded("bgx_dma_copy_d2h", [&]() -> int {
+        if (!h_dst || !d_src || !ticket) return fail(BGX_E_ARG, "bgx_dma_copy_d2h: null pointer");
+        *ticket = 0;
+        if (bytes == 0) return BGX_OK;
+        DmaDev* d = nullptr;
+        if (int rc = dma_setup(device, &d)) return rc;
+        void* dst = nullptr;   // the device-visible address of the page-locked host range
+        HIP_TRY(hipHostGetDevicePointer(&dst, h_dst, 0));
+        hsa_signal_t sig;
+        if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+            return fail(BGX_E_STATE, "bgx_dma_copy_d2h: hsa_signal_create failed");
+        const hsa_status_t st = hsa_amd_memory_async_copy_on_engine(dst, d->cpu, d_src, d->gpu, (size_t)bytes, 0,
+                                                                    nullptr, sig, d->engine, true);
+        if (st != HSA_STATUS_SUCCESS) {
+            hsa_signal_destroy(sig);
+            return fail(BGX_E_STATE, "bgx_dma_copy_d2h: hsa_amd_memory_async_copy_on_engine failed (%d)", (int)st);
+        }
+        *ticket = sig.handle;
+        return BGX_OK;
+    });
+}
+
+int bgx_dma_wait(uint64_t ticket, int timeout_ms) {
+    return guarded("bgx_dma_wait", [&]() -> int {
+        if (ticket == 0) return BGX_OK;
+        hsa_signal_t sig;
+        sig.handle = ticket;
+        const uint64_t ns = timeout_ms > 0 ? (uint64_t)timeout_ms * 1000000ull : UINT64_MAX;
+        const hsa_signal_value_t v =
+            hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, ns, HSA_WAIT_STATE_BLOCKED);
+        if (v >= 1) return fail(BGX_E_STATE, "bgx_dma_wait: copy not finished after %d ms", timeout_ms);
+        hsa_signal_destroy(sig);
         return BGX_OK;
     });
 }

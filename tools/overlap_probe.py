@@ -35,7 +35,7 @@ for i in range(12):
     if pend_t is not None:
         h = e.harvest_fetch(pend_t)
         n_bytes += h.n_episodes * 64 + h.n_records * 48
-        inflight = g.publish(h)              # DMA copy, concurrent with the launch just queued
+        inflight = g.publish(h, ready=True)  # DMA copy, concurrent with the launch just queued
     pend_t = t
 if inflight is not None:
     inflight.wait()
