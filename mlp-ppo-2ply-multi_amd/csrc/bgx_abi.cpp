@@ -841,6 +841,13 @@ int bgx_engine_destroy(bgx_engine* e) {
                 fprintf(stderr, "[bgx fused prof] tier-1 wait for the last-round lanes: %.2f us, queue pop to expansion "
                         "%.2f us per wave-step (pop + lane %.2f, words + root %.2f)\n", s[19] / nws / 100, s[20] / nws / 100,
                         s[21] / nws / 100, s[22] / nws / 100);
+                {
+                    double c[3] = {0, 0, 0};
+                    for (int b = 0; b < 1024; ++b)
+                        for (int k = 0; k < 3; ++k) c[k] += (double)p[(size_t)b * 32 + 29 + k];
+                    fprintf(stderr, "[bgx fused prof] choice per wave-step: state + Philox refill %.2f, pick %.2f, "
+                            "env step %.2f us\n", c[0] / nws / 100, c[1] / nws / 100, c[2] / nws / 100);
+                }
                 fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
                         s[11] / (s[12] > 0 ? s[12] : 1) / 100);
                 fprintf(stderr, "[bgx fused prof] tier-1 job: doubles %.2f us (%.0f jobs), non-doubles %.2f us (%.0f jobs)\n",

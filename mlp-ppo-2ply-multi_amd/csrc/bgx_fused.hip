@@ -13,9 +13,10 @@
 //   2. the LDS that held the slices takes the split-fp16 W fragments, and the
 //      workgroup's rows (the lanes' obs rows + candidates, ~340 per step) are
 //      staged behind them;
-//   3. value MLP in (32-board tile, 32-hidden m-tile) items spread over the
-//      waves (mlp_item; partials summed in the canonical epilogue order, so V
-//      has the same bits as the phased engine's) — V lands in LDS;
+//   3. value MLP in 32-board tile items spread over the waves, all four
+//      32-hidden m-tiles of a tile in one wave (mlp_tile4; the canonical
+//      epilogue order, so V has the same bits as the phased engine's) — V
+//      lands in LDS;
 //   4. each wave samples its lanes' actions from softmax(V/T) and runs the env
 //      step (lane_advance: apply, rewards, record, reset) on the lane state,
 //      which stays in LDS for the whole launch.
@@ -66,7 +67,7 @@ template <int FL> struct FCfg {
     static constexpr int CP_F = 128 * NW;
     static_assert(sizeof(CoopPathLds<NW, CP_F>) <= F_SCR, "path expansion fits the scratch");
     static constexpr int F_TAIL = F_W + NFRAG * 16;
-    static constexpr int FT = F_SCR / (4 * 64 * 4 + 32 * 32);   // MLP tiles per batch: partials + staged rows
+    static constexpr int FT = F_SCR / (32 * 32);   // MLP tiles per batch: staged rows (32 B per board)
     // V(s), V(candidates 0..XS-2) of each lane kept in LDS (the rest: vbuf): as many as fit (<= 96)
     static constexpr int XS_FIT = (160 * 1024 - F_TAIL - (int)sizeof(FusedTail<FL>)) / (FL * 4);
     static constexpr int XS = XS_FIT < 96 ? XS_FIT : 96;
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     unsigned long long twb = 0;                 // tier-1 clocks spent waiting for the last-round lanes
     unsigned long long tpre = 0;                // tier-1 clocks from a job's queue pop to its expansion
     unsigned long long tpa = 0, tpm = 0;        // ... of which: queue pop + lane lookup, job words + root analysis
+    unsigned long long tcs[3] = {0, 0, 0};      // choice: state + Philox refill, pick, env step (lane_advance)
     constexpr bool prof = PROF;
     auto tick = [&](int k) {
         if (prof && t == 0) {
@@ -131,8 +133,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             tc = c;
         }
     };
-    float* vp = (float*)lds;                           // [4][FT][64] MLP partials (scratch)
-    uint4* rs = (uint4*)(lds + 4 * FT * 64 * 4);       // [FT * 32][2] staged rows (scratch)
+    uint4* rs = (uint4*)lds;                           // [FT * 32][2] staged rows (scratch)
     const int groups = (e.L + FL - 1) / FL;
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int nlive = e.L - g * FL < FL ? e.L - g * FL : FL;
@@ -366,49 +367,26 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             if (n_tiles == 0 && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // no MLP batch this step
             __syncthreads();
             tick(2);
-            // ---- 4. value MLP: (32-board tile, m-tile) items over the waves,
-            // partials combined in the canonical epilogue order (bgx_mlp.h)
+            // ---- 4. value MLP: one 32-board tile per item, all four m-tiles in
+            // the wave (mlp_tile4: the feature fragment built once per k-step; V
+            // complete in the wave in the canonical epilogue order, bgx_mlp.h)
             const unsigned long long m0 = prof ? wall_clock64() : 0ull;
             for (int tb = 0; tb < n_tiles; tb += FT) {
                 const int nt = n_tiles - tb < FT ? n_tiles - tb : FT;
-                // items: (tile pair, m-tile); an odd last tile runs alone
-                const int npair = (nt + 1) >> 1;
                 const unsigned long long i0 = prof ? wall_clock64() : 0ull;
-                for (int it = w; it < 4 * npair; it += NW) {
-                    const int tp = it >> 2, m = it & 3;
-                    const int t0 = 2 * tp, c0 = t0 * 32 + (l & 31);
-                    const uint4 bx0 = rs[2 * c0], by0 = rs[2 * c0 + 1];
-                    if (t0 + 1 < nt) {
-                        const int c1 = c0 + 32;
-                        const uint4 bx1 = rs[2 * c1], by1 = rs[2 * c1 + 1];
-                        float p0, p1;
-                        mlp_item2(wf, T.lut, T.w2s, f.feat_scale, bx0, by0, bx1, by1,
-                                  tile_kmask(bx0, by0) | tile_kmask(bx1, by1), m, p0, p1);
-                        vp[(m * FT + t0) * 64 + l] = p0;
-                        vp[(m * FT + t0 + 1) * 64 + l] = p1;
-                    } else {
-                        vp[(m * FT + t0) * 64 + l] =
-                            mlp_item(wf, T.lut, T.w2s, f.feat_scale, bx0, by0, tile_kmask(bx0, by0), m);
+                for (int it = w; it < nt; it += NW) {
+                    const int c0 = it * 32 + (l & 31);
+                    const uint4 bx = rs[2 * c0], by = rs[2 * c0 + 1];
+                    const float v = mlp_tile4(wf, T.lut, T.w2s, f.feat_scale, bx, by, tile_kmask(bx, by));
+                    const int r = (tb + it) * 32 + l;
+                    if (l < 32 && r < nr) {
+                        const float val = v + f.b2;
+                        const int vl = lane_of(r), k = r - T.pre[vl];
+                        if (k < XS) xs[vl * XS + k] = val;
+                        else f.vbuf[(size_t)(g * FL + vl) * (f.cap + 1) + k] = val;
                     }
                 }
                 if (prof) tw[1] += wall_clock64() - i0;   // the wave's MLP items (no barrier)
-                __syncthreads();
-                for (int c = t; c < nt * 32; c += NT) {
-                    const int tl = c >> 5, col = c & 31;
-                    const int r = (tb + tl) * 32 + col;
-                    if (r < nr) {
-                        float vh[2];
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int q = tl * 64 + col + 32 * h;
-                            vh[h] = ((vp[q] + vp[FT * 64 + q]) + vp[2 * FT * 64 + q]) + vp[3 * FT * 64 + q];
-                        }
-                        const float val = (vh[0] + vh[1]) + f.b2;
-                        const int v = lane_of(r), k = r - T.pre[v];
-                        if (k < XS) xs[v * XS + k] = val;
-                        else f.vbuf[(size_t)(g * FL + v) * (f.cap + 1) + k] = val;
-                    }
-                }
                 if (tb + FT >= n_tiles && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // the last batch
                 __syncthreads();
                 if (tb + FT < n_tiles) {
@@ -438,6 +416,12 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 rng.ctr = sr.ctr;
                 rng.dt = lane_dice(e, i);
                 rng.refill();
+                unsigned long long c0 = 0;
+                if (prof) {
+                    __builtin_amdgcn_s_waitcnt(0);
+                    c0 = wall_clock64();
+                    tcs[0] += c0 - s1;
+                }
                 if (n <= 0) {
                     lane_advance(e, i, sr, rng, -1, sr.w, 0.0f, 0.0f, 0, lead);
                 } else {
@@ -450,7 +434,12 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             ? pick_action_half([&](int k) { return xv[1 + k] / Tm; }, n, e.greedy != 0, u)
                             : pick_action_half([&](int k) { return (1 + k < XS ? xv[1 + k] : vv[1 + k]) / Tm; }, n,
                                                e.greedy != 0, u);
-                    if (prof) tw[2] += wall_clock64() - s1;
+                    if (prof) {
+                        const unsigned long long c1 = wall_clock64();
+                        tw[2] += c1 - s1;
+                        tcs[1] += c1 - c0;
+                        c0 = c1;
+                    }
                     uint32_t nb[8];
                     const int r = T.pre[v] + 1 + pick;
                     if (nr <= FT * 32 && !last) {
@@ -462,6 +451,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     }
                     const float va = 1 + pick < XS ? xv[1 + pick] : vv[1 + pick];
                     lane_advance(e, i, sr, rng, pick, nb, xv[0], va, n_full, lead);
+                    if (prof) {
+                        __builtin_amdgcn_s_waitcnt(0);
+                        tcs[2] += wall_clock64() - c0;
+                    }
                 }
                 wave_sync();
                 if (lead) T.st[v] = sr;
@@ -506,6 +499,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             atomicAdd(P + 20, tpre);
             atomicAdd(P + 21, tpa);
             atomicAdd(P + 22, tpm);
+            for (int k = 0; k < 3; ++k) atomicAdd(P + 29 + k, tcs[k]);
         }
     }
     if (t == 0) {

@@ -174,4 +174,52 @@ BGX_DEV void mlp_item2(const uint4* wf, const uint4* lut, const float* w2s, floa
     p1 = q1;
 }
 
+// One 32-board tile through all four m-tiles on one wavefront (the fused
+// kernel's MLP items): a k-step's feature fragment is built once and feeds its
+// eight MFMAs (four m-tiles x hi / lo), and V is complete in the wave, in the
+// canonical epilogue order (p_m per m-tile, v_h = ((p_0 + p_1) + p_2) + p_3,
+// V = (v_0 + v_1) + b2 on the lanes of half 0), so it has the bits of every
+// other MLP kernel. kmask: the tile's nonzero k-steps (tile_kmask). Returns
+// v_0 + v_1 (the caller adds b2) on lanes 0..31.
+BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx, uint4 by,
+                        uint32_t kmask) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int h = lane >> 5;
+    floatx16 acc[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[m][r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+        if (kmask & (1u << s)) {
+            const half8 b = feat_frag(bx, by, s, h, lut, fs);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint4 ah = wf[((0 * 4 + m) * KSTEPS + s) * 64 + lane];
+                const uint4 al = wf[((1 * 4 + m) * KSTEPS + s) * 64 + lane];
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, b, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, b, acc[m], 0, 0, 0);
+            }
+        }
+    }
+    float v = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float p = 0.0f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
+            const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float ex = __builtin_amdgcn_exp2f(acc[m][4 * g + k]);
+                p = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), p);
+            }
+        }
+        v = m == 0 ? p : v + p;
+    }
+    return v + __shfl_xor(v, 32, 64);
+}
+
 }  // namespace bgx
