@@ -321,25 +321,26 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
     for (int i = t; i < e.L; i += 1024) e.harv[i] = e.ep_first[i];
 }
 
-// harvest, step 2: copy finished episodes' records out of the lane rings,
-// 16 bytes per thread (a record is three uint4; persistent grid; the episode
-// count comes from harvest_scan_kernel)
+// harvest, step 2: copy finished episodes' headers and records out of the
+// lane rings, one wavefront per episode (four per 256-thread block, so 4,096
+// episodes are in flight at once), 16 bytes per lane (a record is three
+// uint4); persistent grid; the episode count comes from harvest_scan_kernel
 __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
                                                      const int32_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ info, uint32_t* __restrict__ hout,
                                                      uint32_t* __restrict__ out) {
     const int n_eps = (int)info[0];
     constexpr int Q = REC_WORDS / 4;
-    for (int ep = blockIdx.x; ep < n_eps; ep += gridDim.x) {
+    const int wpb = (int)blockDim.x >> 6, l = lane_id();
+    for (int ep = blockIdx.x * wpb + ((int)threadIdx.x >> 6); ep < n_eps; ep += gridDim.x * wpb) {
         const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
         // the header too: the episode list is refilled by the next step
-        if (threadIdx.x < EP_WORDS / 4)
-            ((uint4*)(hout + (size_t)ep * EP_WORDS))[threadIdx.x] = ((const uint4*)h)[threadIdx.x];
+        if (l < EP_WORDS / 4) ((uint4*)(hout + (size_t)ep * EP_WORDS))[l] = ((const uint4*)h)[l];
         const int lane = (int)h[0] - e.lane_base;
         const uint32_t first = h[2], nrec = h[3];
         const uint4* src = (const uint4*)(e.ring + (size_t)lane * e.R * REC_WORDS);
         uint4* dst = (uint4*)(out + (size_t)offs[ep] * REC_WORDS);
-        for (uint32_t q = threadIdx.x; q < nrec * Q; q += blockDim.x) {
+        for (uint32_t q = (uint32_t)l; q < nrec * Q; q += 64) {
             const uint32_t r = q / Q, k = q - r * Q;
             const uint32_t slot = (first + r) & (uint32_t)(e.R - 1);
             dst[q] = src[slot * Q + k];

@@ -169,3 +169,62 @@ def test_host_gather_world2_real_harvests(weights_seed0):
         for key in ref:
             np.testing.assert_array_equal(merged[key][0], ref[key][0], err_msg=str(key))
             np.testing.assert_array_equal(merged[key][1], ref[key][1], err_msg=str(key))
+
+
+def _nccl_rank(rank, world, port, L, steps, out):
+    import sys
+    from conftest import PKG, golden
+    sys.path.insert(0, PKG)
+    import torch
+    import torch.distributed as dist
+    from bgx import Engine
+    from bgx import dist as bdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    w = {k: golden("weights_seed0.npz")[k] for k in ("W1", "b1", "w2", "b2")}
+    w = bdist.broadcast_weights(w, src=0)
+    base, n = bdist.lane_block(rank, L)
+    e = Engine(lanes=n, lane_base=base, seed=17)
+    e.set_weights(w, 1.5, 1)
+    e.step(steps)
+    h = e.harvest()
+    if rank == 1:   # a rank with nothing to send: the gather skips its point-to-point ops
+        from bgx.engine import Harvest
+        h = Harvest(h.headers[:0], h.records[:0])
+    res = bdist.gather_episodes(h, dst=0, keep=True, async_op=True).wait()
+    if rank == 0:
+        out.put([(hh.cpu().numpy().view(np.uint32), rr.cpu().numpy().view(np.uint32)) for hh, rr in res[2]])
+    e.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_nccl_world2_gather_with_an_empty_rank(weights_seed0):
+    """The RCCL (nccl backend) branch of bgx.dist.gather_episodes on two GPUs,
+    device-side counts and buffers, with one rank sending nothing.
+    Needs >= 2 visible GPUs (the driver's 8-GPU node); skipped on one."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    from bgx import Engine
+    L, steps = 128, 120
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_nccl_rank, args=(r, 2, port, L, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    e = Engine(lanes=L, seed=17)   # rank 0's lane block on its own
+    e.set_weights(weights_seed0, 1.5, 1)
+    e.step(steps)
+    h = e.harvest()
+    e.close()
+    assert len(got) == 2 and got[1][0].shape[0] == 0 and got[1][1].shape[0] == 0
+    np.testing.assert_array_equal(got[0][0], h.headers.cpu().numpy().view(np.uint32))
+    np.testing.assert_array_equal(got[0][1], h.records.cpu().numpy().view(np.uint32))
