@@ -142,9 +142,10 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
 
         def consume(t):
             nonlocal inflight
-            h = eng.harvest_fetch(t)
             if world == 1:
+                eng.harvest_fetch(t, wrap=False)   # the harvest ran on the device; nobody reads it here
                 return
+            h = eng.harvest_fetch(t)
             if hg is not None:      # DMA engines into host shared memory; no collective
                 seq[0] += 1
                 if rank == 0:

@@ -114,12 +114,15 @@ class Engine:
         check(lib().bgx_harvest_enqueue(self._h, ctypes.byref(t), stream_handle(stream)), "bgx_harvest_enqueue")
         return int(t.value)
 
-    def harvest_fetch(self, ticket: int, clone=False) -> Harvest:
+    def harvest_fetch(self, ticket: int, clone=False, wrap=True):
         """Wait for a queued harvest (one of the last two tickets). Without
         clone the tensors alias the engine's buffers, valid until the second
-        harvest_enqueue after `ticket`."""
+        harvest_enqueue after `ticket`. wrap=False returns only the counts
+        (n_episodes, n_records), for a caller that does not read the records."""
         info = HarvestInfo()
         check(lib().bgx_harvest_fetch(self._h, int(ticket), ctypes.byref(info)), "bgx_harvest_fetch")
+        if not wrap:
+            return int(info.n_episodes), int(info.n_records)
         return self._harvest_from(info, clone)
 
     def _harvest_from(self, info, clone):

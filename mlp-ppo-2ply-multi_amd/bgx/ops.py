@@ -129,11 +129,13 @@ class Net:
         check(lib().bgx_net_create(_fp(W1), _fp(b1), _fp(w2), _fp(b2), ctypes.byref(h)),
               "bgx_net_create")
         self._h = h
+        self._destroy = lib().bgx_net_destroy   # bound now: module globals are gone at interpreter exit
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h and h.value:
-            lib().bgx_net_destroy(h)
+        destroy = getattr(self, "_destroy", None)
+        if h and h.value and destroy is not None:
+            destroy(h)
             self._h = None
 
     def value(self, x, stream=None):

@@ -205,10 +205,18 @@ BGX_DEV bool small_double(int j) {   // DICE_ROLLS index 0 = 1-1, 6 = 2-2, 11 = 
 
 // 2-ply: per (candidate, roll) job, mean of the top-5 reply values
 // (two_ply.py:133-142); 0 when the opponent has no move (the roll adds nothing).
-// 16 lanes per job (coalesced loads); each lane keeps its top 5, then five
-// group-max rounds pop the job's top 5 in descending order (the reference's
-// summation order). sample_k > 0: the reference-sampled mode above, keyed by
-// skey and the step salt *salt_dev (null: 0).
+// A wave takes 16 jobs per iteration, 4 lanes per job: a lane reads the job's
+// values k = gl, gl + 4, ... eight loads at a time (issued together) and keeps
+// its top 5 with a max / min network; five group-max rounds then pop the
+// job's top 5 in descending order (the reference's summation order). The
+// lanes of a wave run in lock step, so an iteration costs what its largest job
+// costs: the 16 jobs of an iteration are one roll of 16 consecutive
+// candidates (jobs (16 b + i) * 21 + r), whose reply counts are alike, not 16
+// consecutive rolls of one candidate (a 1-1 with hundreds of replies beside
+// fifteen rolls of a dozen). sample_k > 0: the reference-sampled mode above,
+// keyed by skey and the step salt *salt_dev (null: 0).
+constexpr int T5_GL = 4;
+constexpr int T5_B = 8;    // loads in flight per lane
 __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    const int32_t* __restrict__ job_off,
                                                    const int32_t* __restrict__ job_cnt, int n_jobs,
@@ -216,50 +224,76 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    int jobs_per_unit, int max_jobs, float* __restrict__ out,
                                                    int sample_k, uint64_t skey,
                                                    const unsigned long long* __restrict__ salt_dev) {
+    constexpr int JW = 64 / T5_GL;   // jobs per wave iteration
     int nj = n_jobs;
     if (n_units_dev) nj += (int)(*n_units_dev) * jobs_per_unit;
     if (nj > max_jobs) nj = max_jobs;
     const unsigned long long salt = (sample_k > 0 && salt_dev) ? *salt_dev : 0ull;
-    const int gl = lane_id() & 15, q = lane_id() >> 4;
+    const int gl = lane_id() & (T5_GL - 1), q = lane_id() / T5_GL;
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int n_waves = (int)((gridDim.x * blockDim.x) >> 6);
-    // a wave takes 4 consecutive jobs per iteration; all its lanes stay in the
-    // loop (group shuffles), lanes of jobs past nj are inert
-    for (int jb = 4 * wave; jb < nj; jb += 4 * n_waves) {
-        const int j = jb + q;
+    // iteration it -> (candidate block b, roll r); jobs past nj are inert
+    const int n_cand = (nj + 20) / 21;
+    const int n_it = ((n_cand + JW - 1) / JW) * 21;
+    auto job_of = [&](int it) { return (JW * (it / 21) + q) * 21 + it % 21; };
+    int itr = wave;
+    int cn = 0, on = 0;
+    if (itr < n_it) {
+        const int j0 = job_of(itr);
+        if (j0 < nj) {
+            cn = job_cnt[j0];
+            on = job_off[j0];
+        }
+    }
+    for (; itr < n_it; itr += n_waves) {
+        const int j = job_of(itr);
         const bool live = j < nj;
-        int c = live ? job_cnt[j] : 0;
-        const int o = live ? job_off[j] : 0;
+        int c = live ? cn : 0;
+        const int o = on;
+        if (itr + n_waves < n_it) {   // next iteration's job
+            const int jn = job_of(itr + n_waves);
+            if (jn < nj) {
+                cn = job_cnt[jn];
+                on = job_off[jn];
+            }
+        }
         const bool samp = sample_k > 0 && c > sample_k && c <= 1024 && small_double(j);
         u32x4 pk = {0u, 0u, 0u, 0u};
         if (samp) pk = philox(skey, 0x2B1A000000000000ull ^ salt, (uint64_t)j);
         float t[5] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        for (int k = gl; k < c; k += 16) {
-            if (samp && perm_below((uint32_t)k, (uint32_t)c, pk) >= (uint32_t)sample_k) continue;
-            const float v = V[o + k];
-            if (!(v > t[4])) continue;
-            if (v > t[0]) { t[4] = t[3]; t[3] = t[2]; t[2] = t[1]; t[1] = t[0]; t[0] = v; }
-            else if (v > t[1]) { t[4] = t[3]; t[3] = t[2]; t[2] = t[1]; t[1] = v; }
-            else if (v > t[2]) { t[4] = t[3]; t[3] = t[2]; t[2] = v; }
-            else if (v > t[3]) { t[4] = t[3]; t[3] = v; }
-            else { t[4] = v; }
+        for (int k0 = gl; k0 < c; k0 += T5_B * T5_GL) {
+            float xv[T5_B];
+#pragma unroll
+            for (int u = 0; u < T5_B; ++u) {
+                const int k = k0 + T5_GL * u;
+                const bool use = k < c && !(samp && perm_below((uint32_t)k, (uint32_t)c, pk) >= (uint32_t)sample_k);
+                xv[u] = use ? V[o + k] : -INFINITY;
+            }
+            // branch-free insert (a max / min network): t stays the lane's top 5
+            // in descending order; equal values are interchangeable in the sum
+#pragma unroll
+            for (int u = 0; u < T5_B; ++u) {
+                float v = xv[u];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    const float hi = fmaxf(t[i], v);
+                    v = fminf(t[i], v);
+                    t[i] = hi;
+                }
+            }
         }
         if (samp) c = sample_k;   // the replies kept
         const int m = c < 5 ? c : 5;
         float s = 0.0f;
         for (int r = 0; r < 5; ++r) {
-            // the group's largest head: a DPP max-scan inside the 16-lane row
-            // (lane 15 of the row ends with the row's max), read back with one
-            // shuffle; the lowest lane holding it pops (ties: lower lane first)
+            // the group's largest head (xor-shuffle max over the 4 lanes); the
+            // lowest lane holding it pops (ties: lower lane first)
             float mx = t[0];
-            mx = dpp_maxf<0x111, 0xF>(mx);
-            mx = dpp_maxf<0x112, 0xF>(mx);
-            mx = dpp_maxf<0x114, 0xF>(mx);
-            mx = dpp_maxf<0x118, 0xF>(mx);
-            const float v = __shfl(mx, (lane_id() & 48) | 15, 64);
-            const uint32_t grp = (uint32_t)(ballot(t[0] == v) >> (16 * q)) & 0xFFFFu;
+            mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+            const uint32_t grp = (uint32_t)(ballot(t[0] == mx) >> (T5_GL * q)) & ((1u << T5_GL) - 1u);
             const int who = __ffs(grp) - 1;
-            if (r < m) s = r ? s + v : v;
+            if (r < m) s = r ? s + mx : mx;
             if (who == gl) { t[0] = t[1]; t[1] = t[2]; t[2] = t[3]; t[3] = t[4]; t[4] = -INFINITY; }
         }
         if (live && gl == 0) out[j] = m ? s / (float)m : 0.0f;
@@ -368,8 +402,8 @@ extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, co
                                       int max_jobs, float* out, int sample_k, uint64_t skey,
                                       const unsigned long long* salt_dev, hipStream_t stream) {
     if (max_jobs <= 0) return hipSuccess;
-    int blocks = (max_jobs + 15) / 16;   // 16 jobs per 256-thread block
-    if (blocks > 8192) blocks = 8192;
+    int blocks = (max_jobs + 4 * 16 - 1) / (4 * 16);   // 16 jobs per wave, 4 waves per block
+    if (blocks > 2048) blocks = 2048;                   // 8 waves per SIMD on 256 CUs, then loop
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
                        n_units_dev, jobs_per_unit, max_jobs, out, sample_k, skey, salt_dev);
     return hipGetLastError();

@@ -50,6 +50,8 @@ template <int FL> struct FusedTail {
     int next[2];                    // tier-1 job counters, alternating by step parity
     int bdone;                      // last-round lanes stepped so far (this group; see OVL)
     int go[2];                      // step s runs iff go[s & 1] (the balanced launch's tickets)
+    int qnext;                      // the merged MLP + choice phase's item counter
+    unsigned tdone[64];             // MLP tile t of this step is written iff tdone[t] == the step's tag
     int pre[FL + 1];                // MLP row prefix over the lanes
     uint32_t job[FL][8];            // the lanes' jobs: packed board words 0..6, player | d0 << 8 | d1 << 16
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
@@ -68,6 +70,7 @@ template <int FL> struct FCfg {
     static_assert(sizeof(CoopPathLds<NW, CP_F>) <= F_SCR, "path expansion fits the scratch");
     static constexpr int F_TAIL = F_W + NFRAG * 16;
     static constexpr int FT = F_SCR / (32 * 32);   // MLP tiles per batch: staged rows (32 B per board)
+    static_assert(FT <= 64, "a tile flag per staged tile (FusedTail::tdone)");
     // V(s), V(candidates 0..XS-2) of each lane kept in LDS (the rest: vbuf): as many as fit (<= 96)
     static constexpr int XS_FIT = (160 * 1024 - F_TAIL - (int)sizeof(FusedTail<FL>)) / (FL * 4);
     static constexpr int XS = XS_FIT < 96 ? XS_FIT : 96;
@@ -100,6 +103,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     const int t = (int)threadIdx.x, w = t >> 6, l = lane_id();
     for (int i = t; i < 256; i += NT) T.lut[i] = lut_entry((uint32_t)i, f.feat_scale);
     for (int i = t; i < 128; i += NT) T.w2s[i] = f.rowc[i];
+    for (int i = t; i < 64; i += NT) T.tdone[i] = 0u;
+    unsigned qtag = 0u;   // this workgroup's step counter (tags tdone; never 0 on a live step)
     uint4* wl = (uint4*)(lds + F_W);     // split-fp16 W fragments, loaded once
     for (int k = t; k < NFRAG; k += NT) wl[k] = f.wfrag[k];
     const uint4* wf = wl;
@@ -361,49 +366,11 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     rs[2 * c + 1] = by;
                 }
             };
-            // ---- 3. the first batch's rows into the scratch
-            const int n_tiles = (nr + 31) >> 5;
-            stage(0, n_tiles < FT ? n_tiles : FT);
-            if (n_tiles == 0 && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // no MLP batch this step
-            __syncthreads();
-            tick(2);
-            // ---- 4. value MLP: one 32-board tile per item, all four m-tiles in
-            // the wave (mlp_tile4: the feature fragment built once per k-step; V
-            // complete in the wave in the canonical epilogue order, bgx_mlp.h)
-            const unsigned long long m0 = prof ? wall_clock64() : 0ull;
-            for (int tb = 0; tb < n_tiles; tb += FT) {
-                const int nt = n_tiles - tb < FT ? n_tiles - tb : FT;
-                const unsigned long long i0 = prof ? wall_clock64() : 0ull;
-                for (int it = w; it < nt; it += NW) {
-                    const int c0 = it * 32 + (l & 31);
-                    const uint4 bx = rs[2 * c0], by = rs[2 * c0 + 1];
-                    const float v = mlp_tile4(wf, T.lut, T.w2s, f.feat_scale, bx, by, tile_kmask(bx, by));
-                    const int r = (tb + it) * 32 + l;
-                    if (l < 32 && r < nr) {
-                        const float val = v + f.b2;
-                        const int vl = lane_of(r), k = r - T.pre[vl];
-                        if (k < XS) xs[vl * XS + k] = val;
-                        else f.vbuf[(size_t)(g * FL + vl) * (f.cap + 1) + k] = val;
-                    }
-                }
-                if (prof) tw[1] += wall_clock64() - i0;   // the wave's MLP items (no barrier)
-                if (tb + FT >= n_tiles && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // the last batch
-                __syncthreads();
-                if (tb + FT < n_tiles) {
-                    stage(tb + FT, n_tiles - tb - FT < FT ? n_tiles - tb - FT : FT);
-                    __syncthreads();
-                }
-            }
-            if (prof) tw[0] += wall_clock64() - m0;
-            tick(3);
-            // ---- 5. action choice + env step for the wave's lanes (the chosen
-            // afterstate is still staged in LDS when the step fit one MLP batch)
-            // (two of the wave's lanes side by side, one per half-wave)
-#pragma unroll 1
-            for (int pr = 0; pr < PR; ++pr) {
-                const bool last = OVL && pr == PR - 1;
-                if (last) __syncthreads();   // the staged rows are the next step's slices from here on
-                const int v = 2 * (pr * NW + w) + (l >> 5);
+            // ---- 5 (body). action choice + env step of lane v (the chosen
+            // afterstate is still staged in LDS when the step fit one MLP batch
+            // and this is not the OVL round); two of a wave's lanes side by side,
+            // one per half-wave
+            auto choose = [&](int v, bool last) {
                 const bool lead = (l & 31) == 0;
                 if (v < nlive) {
                 const int i = g * FL + v;
@@ -464,6 +431,107 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 }
                 if (prof) tw[3] += wall_clock64() - s1;
                 }
+            };
+            // one MLP tile (32 rows) of batch tb: V into the lanes' values
+            auto mlp_one = [&](int tb, int it) {
+                const int c0 = it * 32 + (l & 31);
+                const uint4 bx = rs[2 * c0], by = rs[2 * c0 + 1];
+                const float v = mlp_tile4(wf, T.lut, T.w2s, f.feat_scale, bx, by, tile_kmask(bx, by));
+                const int r = (tb + it) * 32 + l;
+                if (l < 32 && r < nr) {
+                    const float val = v + f.b2;
+                    const int vl = lane_of(r), k = r - T.pre[vl];
+                    if (k < XS) xs[vl * XS + k] = val;
+                    else f.vbuf[(size_t)(g * FL + vl) * (f.cap + 1) + k] = val;
+                }
+            };
+            // ---- 3. the first batch's rows into the scratch
+            const int n_tiles = (nr + 31) >> 5;
+            // one batch (the usual case): the MLP tiles and the choice phase's
+            // first round are one item queue (below)
+#ifdef BGX_NO_MERGE
+            const bool merged = false;   // A/B builds: barrier-separated MLP and choice phases
+#else
+            const bool merged = n_tiles <= FT;
+#endif
+            stage(0, n_tiles < FT ? n_tiles : FT);
+            if (t == 0) T.qnext = NW;
+            if (n_tiles == 0 && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // no MLP batch this step
+            ++qtag;
+            __syncthreads();
+            tick(2);
+            const unsigned long long m0 = prof ? wall_clock64() : 0ull;
+            if (merged) {
+                // ---- 4 + 5a. value MLP and the first choice round as one queue:
+                // items 0 .. n_tiles - 1 are the MLP tiles (one 32-board tile per
+                // item, all four m-tiles in the wave: mlp_tile4), then one item per
+                // pair of first-round lanes. A wave takes item w, then the next from
+                // an LDS counter; a choice item waits (LDS flags, bounded) for the
+                // tiles holding its lanes' rows. Every tile item is handed out before
+                // any choice item and a tile item waits on nothing, so the waits end.
+                // The MFMA-bound tiles and the latency-bound choice chains then share
+                // the SIMDs instead of running in two barrier-separated phases.
+                const int nc0 = (nlive + 1) / 2 < NW ? (nlive + 1) / 2 : NW;   // first-round lane pairs
+                int it = w;
+                while (it < n_tiles + nc0) {
+                    if (it < n_tiles) {
+                        const unsigned long long i0 = prof ? wall_clock64() : 0ull;
+                        mlp_one(0, it);
+                        // the tile's values (LDS and, past XS, vbuf) before its flag
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        if (l == 0) __hip_atomic_store(&T.tdone[it], qtag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (prof) tw[1] += wall_clock64() - i0;
+                    } else {
+                        const int p = it - n_tiles;
+                        const int va = 2 * p, vb = 2 * p + 2 < nlive ? 2 * p + 2 : nlive;
+                        const int r0 = T.pre[va], r1 = T.pre[vb];   // the pair's rows [r0, r1)
+                        if (r1 > r0) {
+                            for (int tt = r0 >> 5; tt <= (r1 - 1) >> 5; ++tt) {
+                                // bounded like every in-kernel wait
+                                for (unsigned spin = 0;
+                                     __hip_atomic_load(&T.tdone[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != qtag;
+                                     ++spin) {
+                                    if (spin >= (1u << 24)) {
+                                        if (l == 0) atomicOr(e.err_flags, BGX_ERRF_WAIT_BOUND);
+                                        break;
+                                    }
+                                    __builtin_amdgcn_s_sleep(1);
+                                }
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        }
+                        choose(2 * p + (l >> 5), false);
+                    }
+                    int kn = 0;
+                    if (l == 0) kn = atomicAdd(&T.qnext, 1);
+                    it = uniform(kn);
+                }
+                // (no barrier here: the OVL round starts with one, and without OVL
+                // the step ends with one)
+                if (n_tiles > 0 && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);
+            } else {
+                // ---- 4. value MLP over FT-tile batches (many rows this step)
+                for (int tb = 0; tb < n_tiles; tb += FT) {
+                    const int nt = n_tiles - tb < FT ? n_tiles - tb : FT;
+                    const unsigned long long i0 = prof ? wall_clock64() : 0ull;
+                    for (int it = w; it < nt; it += NW) mlp_one(tb, it);
+                    if (prof) tw[1] += wall_clock64() - i0;   // the wave's MLP items (no barrier)
+                    if (tb + FT >= n_tiles && t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // the last batch
+                    __syncthreads();
+                    if (tb + FT < n_tiles) {
+                        stage(tb + FT, n_tiles - tb - FT < FT ? n_tiles - tb - FT : FT);
+                        __syncthreads();
+                    }
+                }
+            }
+            if (prof) tw[0] += wall_clock64() - m0;
+            tick(3);
+            // ---- 5. the remaining choice rounds (all of them after a multi-batch MLP)
+#pragma unroll 1
+            for (int pr = merged ? 1 : 0; pr < PR; ++pr) {
+                const bool last = OVL && pr == PR - 1;
+                if (last) __syncthreads();   // the staged rows are the next step's slices from here on
+                choose(2 * (pr * NW + w) + (l >> 5), last);
             }
             // the next step's ticket (written before this step's first barrier):
             // the OVL round's lanes are finished by a barrier before the group ends

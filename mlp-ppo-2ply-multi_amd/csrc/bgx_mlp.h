@@ -9,6 +9,13 @@ namespace bgx {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+// LDS-address-space views: reads through them take a ds_read immediate offset
+// from one base register (a generic pointer would go through flat loads)
+typedef __attribute__((address_space(3))) const v4u* lds_u4p;
+typedef __attribute__((address_space(3))) const float* lds_fp;
 
 constexpr int KSTEPS = 13;   // 208 = 13 x 16 >= 198
 constexpr int NFRAG = 2 * 4 * KSTEPS * 64;
@@ -181,10 +188,20 @@ BGX_DEV void mlp_item2(const uint4* wf, const uint4* lut, const float* w2s, floa
 // V = (v_0 + v_1) + b2 on the lanes of half 0), so it has the bits of every
 // other MLP kernel. kmask: the tile's nonzero k-steps (tile_kmask). Returns
 // v_0 + v_1 (the caller adds b2) on lanes 0..31.
+// Fragments are read through two LDS bases (hi terms, lo terms) with
+// constant offsets below 64 KB; the asm hides the bases from the compiler,
+// which would otherwise fold them into one base plus an address add per read
+// (the fragments sit past the 64 KB an immediate offset reaches).
 BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx, uint4 by,
                         uint32_t kmask) {
     const int lane = (int)(threadIdx.x & 63);
     const int h = lane >> 5;
+    lds_u4p wfh = (lds_u4p)(wf + lane);
+    lds_u4p wfl = (lds_u4p)(wf + 4 * KSTEPS * 64 + lane);
+    lds_fp w2h = (lds_fp)(w2s + 4 * h);
+    asm volatile("" : "+v"(wfh));
+    asm volatile("" : "+v"(wfl));
+    asm volatile("" : "+v"(w2h));
     floatx16 acc[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -196,10 +213,10 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
             const half8 b = feat_frag(bx, by, s, h, lut, fs);
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const uint4 ah = wf[((0 * 4 + m) * KSTEPS + s) * 64 + lane];
-                const uint4 al = wf[((1 * 4 + m) * KSTEPS + s) * 64 + lane];
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, b, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, b, acc[m], 0, 0, 0);
+                const v4u ah = wfh[(m * KSTEPS + s) * 64];
+                const v4u al = wfl[(m * KSTEPS + s) * 64];
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ah), b, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, al), b, acc[m], 0, 0, 0);
             }
         }
     }
@@ -209,7 +226,9 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
         float p = 0.0f;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const float4 c4 = *(const float4*)(w2s + 32 * m + 8 * g + 4 * h);
+            // (read as a float vector: hipcc 7.2 miscompiles bit_cast of the
+            // lanes of a u32 vector loaded from LDS -- every lane became .x)
+            const v4f c4 = *(__attribute__((address_space(3))) const v4f*)(w2h + 32 * m + 8 * g);
             const float cy[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {

@@ -153,68 +153,109 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
     }
 }
 
-// Throughput variant (2 tiles of 32 boards per wave): all 13 feature
-// fragments are built once per tile pair (104 VGPRs), then the four 32-row
-// hidden tiles m run one after another into two alternating accumulator sets;
-// the sigmoid + w2 dot product of tile m-1 is interleaved with tile m's 52
-// MFMAs (the VALU / transcendental issue fits in the MFMA gaps), so only the
-// last tile's epilogue is exposed.
-// rows r0, r0 + 1 (r0 even) of hidden tile m: w2 of j0 = 32m + (r & 3) + 8(r >> 2) + 4h
-// and j0 + 1 are adjacent in LDS (one ds_read_b64)
-BGX_DEV void epi_pair(const floatx16& acc, int m, int r0, int h, const float* w2s, float& v) {
-    const float2 c = *(const float2*)(w2s + 32 * m + (r0 & 3) + 8 * (r0 >> 2) + 4 * h);
+// Throughput kernel (2 tiles of 32 boards per wave, 8 waves, one workgroup per
+// CU): all 13 feature fragments of a tile pair are built once (104 VGPRs),
+// then the four 32-row hidden tiles m run one after another into two
+// alternating accumulator sets; the sigmoid + w2 dot product of tile m-1 runs
+// beside tile m's 52 MFMAs (the VALU / transcendental issue fits in the MFMA
+// gaps). The last m-tile's epilogue is carried into the next tile pair's
+// first m-tile (acc[1] stays live across the iteration), so only each wave's
+// last epilogue is exposed. Each wave's next tile pair of rows is staged
+// global -> LDS by two global_load_lds_dwordx4 (no VGPRs: the kernel is at its
+// register cap) while the current pair's 208 MFMAs run. Same accumulation and
+// epilogue order as every MLP kernel (bgx_mlp.h).
+// (Measured and rejected, DESIGN.md §4: skipping all-zero k-steps -- the
+// branches break the MFMA / epilogue interleave -- and a 12-wave variant that
+// rebuilds the feature fragments per m-tile.)
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef __attribute__((address_space(1))) void* glb_vp;
+
+// epi_pair with the w2 base (w2s + 4 h) as an LDS pointer: the reads take
+// constant offsets from one register
+BGX_DEV void epi_pair_l(const floatx16& acc, int m, int r0, lds_fp w2h, float& v) {
+    const v2f c = *(__attribute__((address_space(3))) const v2f*)(w2h + 32 * m + (r0 & 3) + 8 * (r0 >> 2));
     const float e0 = __builtin_amdgcn_exp2f(acc[r0]), e1 = __builtin_amdgcn_exp2f(acc[r0 + 1]);
     v = fmaf(c.x, __builtin_amdgcn_rcpf(1.0f + e0), v);
     v = fmaf(c.y, __builtin_amdgcn_rcpf(1.0f + e1), v);
 }
+constexpr int IL_NW = 8;
+constexpr int IL_RB = 128;   // uint4 per staged tile pair (64 rows x 32 B)
 
-// (Measured and rejected on the 2-ply reply launch, DESIGN.md §4: loading the
-// next tile pair's rows during this pair's MFMAs, skipping all-zero k-steps --
-// the branches break the MFMA / epilogue interleave -- and a 12-wave variant
-// that rebuilds the feature fragments per m-tile: 903 vs 876 us per launch.)
-__global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
+// rows 64 t .. 64 t + 63 -> dst[2 r], dst[2 r + 1] (wave-uniform LDS base +
+// 16 B per lane); rows past the buffer's capacity read its last row (their
+// V is never stored)
+BGX_DEV void il_stage(const uint32_t* rows, int t, int cap, uint4* dst) {
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int row = 64 * t + 32 * i + (lane >> 1);
+        row = row < cap ? row : cap - 1;
+        const uint4* src = (const uint4*)(rows + (size_t)row * 8) + (lane & 1);
+        __builtin_amdgcn_global_load_lds((glb_vp)(void*)src, (lds_vp)(void*)(dst + 64 * i), 16, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(64 * IL_NW) void mlp_kernel_il(MlpArgs a) {
     constexpr int NT = 2;
     extern __shared__ __attribute__((aligned(16))) uint4 lds[];
     uint4* wf = lds;                                   // [NFRAG]
     uint4* lut = lds + NFRAG;                          // [256]
     float* w2s = (float*)(lds + NFRAG + 256);          // [128] value-head weights
-    for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i, a.feat_scale);
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) w2s[i] = a.rowc[i];
-
+    uint4* rbuf = lds + NFRAG + 256 + 32;              // [IL_NW][2][IL_RB] staged rows
     int n = a.n_rows;
     if (a.n_rows_dev) n += (int)*a.n_rows_dev;
     if (a.n_max > 0 && n > a.n_max) n = a.n_max;
+    const int cap = a.n_max > 0 ? a.n_max : n;
     const int tiles = (n + 32 * NT - 1) / (32 * NT);
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5;
     const int col = lane & 31;
     const int wave = threadIdx.x >> 6;
-    const int NW = blockDim.x >> 6;
-    const int nwaves = gridDim.x * NW;
-    int t = blockIdx.x * NW + wave;
+    const int nwaves = gridDim.x * IL_NW;
+    uint4* rb = rbuf + wave * 2 * IL_RB;
+    // fragment bases: hi terms wf[0 .. 52*64), lo terms from wf + 52*64; each
+    // read then fits a ds_read offset (< 64 KB). The asm (per tile pair) hides
+    // the bases' relation and their loop invariance, so the compiler neither
+    // folds them into one base plus per-fragment address registers nor hoists
+    // the fragment reads out of the loop (into spills).
+    lds_u4p wfh = (lds_u4p)(wf + lane);
+    lds_u4p wfl = (lds_u4p)(wf + 4 * KSTEPS * 64 + lane);
+    lds_fp w2h = (lds_fp)(w2s + 4 * h);
+    int t = blockIdx.x * IL_NW + wave;
+    if (t < tiles) il_stage(a.rows, t, cap, rb);
+    for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i, a.feat_scale);
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) w2s[i] = a.rowc[i];
     __syncthreads();
-    for (; t < tiles; t += nwaves) {
-        // k-steps 0..11 from the LUT, kept in registers; k-step 12 (bars, borne-off,
-        // side to move, bias) is rebuilt from the row word per hidden tile
-        half8 b[KSTEPS - 1][NT];
-        uint32_t w6[NT];
+    float v[NT] = {0.0f, 0.0f}, pm[NT] = {0.0f, 0.0f};   // canonical epilogue order (bgx_mlp.h)
+    floatx16 acc[2][NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[1][q][r] = 0.0f;
+    int tp = -1;   // tile pair whose m-tile 3 accumulators are in acc[1]
+    for (int it = 0; t < tiles; t += nwaves, ++it) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this pair's staged rows landed
+        const uint4* cb = rb + (it & 1) * IL_RB;
+        half8 b[KSTEPS][NT];
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
-            uint4 bx, by;
-            load_rows(a, n, t * NT + q, NT, col, bx, by);
+            const uint4 bx = cb[2 * (32 * q + col)], by = cb[2 * (32 * q + col) + 1];
 #pragma unroll
             for (int s = 0; s < KSTEPS - 1; ++s) b[s][q] = feat_frag(bx, by, s, h, lut, a.feat_scale);
-            w6[q] = by.z;
+            b[KSTEPS - 1][q] = feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, by.z, 0), KSTEPS - 1, h, lut,
+                                         a.feat_scale);
         }
-        float v[NT] = {0.0f, 0.0f}, pm[NT] = {0.0f, 0.0f};   // canonical epilogue order (bgx_mlp.h)
-        floatx16 acc[2][NT];
-        // A pair for (m, s) = (0, 0); each step loads the next pair before its MFMAs
-        uint4 ah = wf[((0 * 4 + 0) * KSTEPS + 0) * 64 + lane];
-        uint4 al = wf[((1 * 4 + 0) * KSTEPS + 0) * 64 + lane];
+        if (t + nwaves < tiles) il_stage(a.rows, t + nwaves, cap, rb + ((it + 1) & 1) * IL_RB);
+        asm volatile("" : "+v"(wfh));
+        asm volatile("" : "+v"(wfl));
+        asm volatile("" : "+v"(w2h));
+        v4u ah = wfh[0];
+        v4u al = wfl[0];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const int cur = m & 1, prv = cur ^ 1;
+            const int mp = m > 0 ? m - 1 : 3;   // m-tile whose epilogue runs beside these MFMAs
 #pragma unroll
             for (int q = 0; q < NT; ++q)
 #pragma unroll
@@ -223,52 +264,59 @@ __global__ __launch_bounds__(512) void mlp_kernel_il(MlpArgs a) {
             for (int s = 0; s < KSTEPS; ++s) {
                 const int mn = s + 1 < KSTEPS ? m : (m + 1 < 4 ? m + 1 : m);
                 const int sn = s + 1 < KSTEPS ? s + 1 : 0;
-                const uint4 nh = wf[((0 * 4 + mn) * KSTEPS + sn) * 64 + lane];
-                const uint4 nl = wf[((1 * 4 + mn) * KSTEPS + sn) * 64 + lane];
+                const v4u nh = wfh[(mn * KSTEPS + sn) * 64];
+                const v4u nl = wfl[(mn * KSTEPS + sn) * 64];
 #pragma unroll
                 for (int q = 0; q < NT; ++q) {
-                    const half8 bq = s < KSTEPS - 1 ? b[s < KSTEPS - 1 ? s : 0][q]
-                                                    : feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, w6[q], 0),
-                                                                KSTEPS - 1, h, lut, a.feat_scale);
-                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&ah, bq, acc[cur][q], 0, 0, 0);
-                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&al, bq, acc[cur][q], 0, 0, 0);
+                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ah), b[s][q], acc[cur][q], 0, 0, 0);
+                    acc[cur][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, al), b[s][q], acc[cur][q], 0, 0, 0);
                 }
-                // tile m-1's epilogue spread over all 13 k-steps: its 16 row
-                // pairs (p: tile p & 1, rows 2 (p >> 1), +1; each tile's rows in
-                // ascending order) two per step in steps 0..2, one per step after
-                if (m > 0) {
-                    const int p_lo = s < 3 ? 2 * s : s + 3;   // s is unrolled: constants
-                    const int p_n = s < 3 ? 2 : 1;
+                // m-tile mp's epilogue spread over the 13 k-steps: its 16 row pairs
+                // (p: tile p & 1, rows 2 (p >> 1), +1; ascending per tile), two
+                // per step in steps 0..2, one per step after
+                const int p_lo = s < 3 ? 2 * s : s + 3;
+                const int p_n = s < 3 ? 2 : 1;
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        if (k >= p_n) break;
-                        const int p = p_lo + k;
-                        epi_pair(acc[prv][p & 1], m - 1, 2 * (p >> 1), h, w2s, pm[p & 1]);
-                    }
-                    if (s == KSTEPS - 1) {
+                for (int k = 0; k < 2; ++k) {
+                    if (k >= p_n) break;
+                    const int p = p_lo + k;
+                    epi_pair_l(acc[prv][p & 1], mp, 2 * (p >> 1), w2h, pm[p & 1]);
+                }
+                if (s == KSTEPS - 1) {
+                    if (m == 0) {
+                        // the previous tile pair is complete: V = (v_0 + v_1) + b2
 #pragma unroll
                         for (int q = 0; q < NT; ++q) {
-                            v[q] = m == 1 ? pm[q] : v[q] + pm[q];
-                            pm[q] = 0.0f;
+                            float vv = v[q] + pm[q];
+                            vv += __shfl_xor(vv, 32, 64);
+                            const int row = (tp * NT + q) * 32 + col;
+                            if (tp >= 0 && h == 0 && row < n) a.out[row] = vv + a.b2;
                         }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < NT; ++q) v[q] = m == 1 ? pm[q] : v[q] + pm[q];
                     }
+#pragma unroll
+                    for (int q = 0; q < NT; ++q) pm[q] = 0.0f;
                 }
                 ah = nh;
                 al = nl;
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+        tp = t;
+    }
+    if (tp >= 0) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2)
 #pragma unroll
-            for (int q = 0; q < NT; ++q) epi_pair(acc[1][q], 3, r, h, w2s, pm[q]);
-#pragma unroll
-        for (int q = 0; q < NT; ++q) v[q] += pm[q];
+            for (int q = 0; q < NT; ++q) epi_pair_l(acc[1][q], 3, r, w2h, pm[q]);
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
-            v[q] += __shfl_xor(v[q], 32, 64);
-            const int row = (t * NT + q) * 32 + col;
-            if (h == 0 && row < n) a.out[row] = v[q] + a.b2;
+            float vv = v[q] + pm[q];
+            vv += __shfl_xor(vv, 32, 64);
+            const int row = (tp * NT + q) * 32 + col;
+            if (h == 0 && row < n) a.out[row] = vv + a.b2;
         }
     }
 }
@@ -314,6 +362,7 @@ __global__ __launch_bounds__(128) void value_f32_kernel(const float* __restrict_
 extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t stream) {
     static int n_cu = 0;
     const int lds = bgx::NFRAG * 16 + 256 * 16 + 128 * 4;
+    const int lds_il = lds + bgx::IL_NW * 2 * bgx::IL_RB * 16;
     if (!n_cu) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -321,7 +370,7 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
             n_cu = 256;
         if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+            hipFuncSetAttribute((const void*)bgx::mlp_kernel_il, hipFuncAttributeMaxDynamicSharedMemorySize, lds_il) !=
                 hipSuccess)
             return hipErrorInvalidValue;
     }
@@ -337,7 +386,7 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
         if (blocks <= 0) return hipSuccess;
     }
     if (nt == 2)
-        hipLaunchKernelGGL(bgx::mlp_kernel_il, dim3(blocks), dim3(512), lds, stream, *args);
+        hipLaunchKernelGGL(bgx::mlp_kernel_il, dim3(blocks), dim3(64 * bgx::IL_NW), lds_il, stream, *args);
     else
         hipLaunchKernelGGL((bgx::mlp_kernel<1, 16>), dim3(blocks), dim3(1024), lds, stream, *args);
     return hipGetLastError();

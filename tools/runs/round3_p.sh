@@ -1,0 +1,27 @@
+# Round-3 session, GPU call 17: MLP tiles and the first choice round as one
+# item queue in the fused kernel (libbgx.so) vs barrier-separated phases
+# (libbgx_nomerge.so, -DBGX_NO_MERGE). Parity first (fused == phased,
+# transitions vs the oracle, replays), then A/B at 20 and 600 steps, prof split.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/r5p2; rm -rf $OUT; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_replay.py -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+for lib in libbgx libbgx_nomerge libbgx libbgx_nomerge; do
+  BGX_LIB=$PWD/mlp-ppo-2ply-multi_amd/bgx/$lib.so timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --two-ply-steps 0 --kall-steps 0 --config1-steps 0 > $OUT/${lib}_20.json 2> $OUT/${lib}_20.err || { tail $OUT/${lib}_20.err; exit 1; }
+  BGX_LIB=$PWD/mlp-ppo-2ply-multi_amd/bgx/$lib.so timeout -k 10 200 python bench.py --steps 600 --warmup 5 --no-cpu-baseline --two-ply-steps 0 --kall-steps 0 --config1-steps 0 > $OUT/${lib}_600.json 2> $OUT/${lib}_600.err || { tail $OUT/${lib}_600.err; exit 1; }
+  python -c "
+import json
+a=json.load(open('$OUT/${lib}_20.json')); b=json.load(open('$OUT/${lib}_600.json'))
+print('$lib', '20:', round(a['value']/1e6,2), '600:', round(b['value']/1e6,2), 'launch600 ms', round(b['kernels']['fused_step']['avg_launch_ms'],3))"
+done
+BGX_FUSED_PROF=1 timeout -k 10 200 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --two-ply-steps 0 --kall-steps 0 --config1-steps 0 > $OUT/prof.json 2> $OUT/prof.err || { tail $OUT/prof.err; exit 1; }
+grep "fused prof" $OUT/prof.err | head -5
+echo "[2-ply] top-5 over aligned 16 B blocks"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $OUT/tests_parity.log 2>&1 || { tail -40 $OUT/tests_parity.log; exit 1; }
+tail -1 $OUT/tests_parity.log
+ARGS="--ply 2 --k-top 4 --steps 100 --warmup 20 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python bench.py $ARGS > $OUT/kt.json 2> $OUT/kt.err || { tail $OUT/kt.err; exit 1; }
+python tools/kstat.py $(find $OUT/kt -name "*kernel_stats.csv" | head -1) "" | head -4
+timeout -k 10 200 python bench.py $ARGS > $OUT/k4.json 2> $OUT/k4.err || { tail $OUT/k4.err; exit 1; }
+python -c "import json; j=json.load(open('$OUT/k4.json')); print('k4', round(j['value']/1e6,3), 'M', round(j['ms_per_step']*1e3,1), 'us/step')"
