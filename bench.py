@@ -314,11 +314,12 @@ def roofline_fused(d, tm):
     901 B per evaluated board) and MLP FLOPs over its average launch.
 
     The kernel is not HBM-bound: fusion keeps features and V on chip, so its
-    physical traffic (PMC) is ~1/28 of the algorithmic bytes, and its counters
-    (VALU ~0.5, MFMA ~0.2 busy, ~44 % of wave-cycles waiting) put it on
-    latency: a chain of phases behind workgroup barriers. `bound` says so;
-    achieved / peak / frac stay the algorithmic-bytes figure of the bench
-    contract, with the physical rate and the busy ratios beside it."""
+    physical traffic (PMC) is ~1/28 of the algorithmic bytes. Each step is one
+    LDS item queue (MLP tiles on MFMA, choice chains, the next step's movegen
+    jobs on VALU + SALU) that the waves of a workgroup share: the bound is
+    issue and dependency latency across those items, not a single unit.
+    `bound` says so; achieved / peak / frac stay the algorithmic-bytes figure
+    of the bench contract, with the physical rate and the busy ratios beside it."""
     el = d["elapsed_s"]
     n = max(1, tm["movegen_launches"])
     launch = tm["movegen_ms"] / n
@@ -335,8 +336,9 @@ def roofline_fused(d, tm):
     m["frac"] = m["achieved"] / m["peak"]
     r = {kk: k[kk] for kk in ("achieved", "peak", "unit", "frac")}
     r["bound"] = "latency"
-    r["bound_detail"] = ("VALU/LDS issue of dependent phases behind workgroup barriers (not HBM: physical "
-                         "traffic below; not MFMA: mfma_busy below)")
+    r["bound_detail"] = ("VALU/SALU issue of the movegen items and dependency latency of the choice items, "
+                         "sharing the SIMDs with the MLP tiles in one queue per step (not HBM: physical traffic "
+                         "below; not MFMA: mfma_busy below)")
     r["kernel"] = "bgx::fused_step_kernel (movegen + encode + MLP + select + env step, all steps of a launch)"
     r["achieved_basis"] = "SURVEY 8d algorithmic bytes (54 B per movegen job + 901 B per evaluated board)"
     # PMC bytes per step of the same workload x the steps of this bench's launches

@@ -831,16 +831,13 @@ int bgx_engine_destroy(bgx_engine* e) {
                     for (int k = 0; k < 23; ++k) s[k] += (double)p[(size_t)b * 32 + k];
                 const double n = s[5] > 0 ? s[5] : 1;
                 const double nws = s[18] > 0 ? s[18] : 1;   // wave-steps
-                fprintf(stderr, "[bgx fused prof] us per workgroup step: step+tier1 %.2f tier2 %.2f wload %.2f mlp %.2f "
-                        "pick %.2f | mean wave tier-1 job %.2f (%0.f workgroup steps)\n",
-                        s[0] / n / 100, s[1] / n / 100, s[2] / n / 100, s[3] / n / 100, s[4] / n / 100,
-                        s[6] / nws / 100, n);
-                fprintf(stderr, "[bgx fused prof] mean per wave-step: mlp %.2f | items %.2f pick %.2f "
-                        "advance %.2f us\n", s[7] / nws / 100, s[8] / nws / 100, s[9] / nws / 100,
-                        s[10] / nws / 100);
-                fprintf(stderr, "[bgx fused prof] tier-1 wait for the last-round lanes: %.2f us, queue pop to expansion "
-                        "%.2f us per wave-step (pop + lane %.2f, words + root %.2f)\n", s[19] / nws / 100, s[20] / nws / 100,
-                        s[21] / nws / 100, s[22] / nws / 100);
+                // (the pipelined kernel: each step is tier 2 + the row prefix, then one item
+                // queue of MLP tiles, choice pairs and the next step's tier-1 jobs)
+                fprintf(stderr, "[bgx fused prof] us per workgroup step: tier2 + prefix %.2f, queue %.2f, end barrier %.2f "
+                        "(%.0f workgroup steps)\n", s[1] / n / 100, s[3] / n / 100, s[4] / n / 100, n);
+                fprintf(stderr, "[bgx fused prof] wave-us per workgroup step in items: MLP tiles %.2f, choice pairs %.2f, "
+                        "tier-1 jobs %.2f (%.2f per wave-step of %d waves)\n", s[8] / n / 100, s[10] / n / 100,
+                        (s[14] + s[16]) / n / 100, (s[8] + s[10] + s[14] + s[16]) / nws / 100, (int)(nws / n + 0.5));
                 {
                     double c[3] = {0, 0, 0};
                     for (int b = 0; b < 1024; ++b)
