@@ -157,6 +157,8 @@ struct bgx_engine {
     bool fused = false;
     uint32_t* fcand = nullptr;
     float* fvbuf = nullptr;
+    int* ft1cnt = nullptr;   // fused: the lanes' next-position expansion counts (FusedArgs::t1cnt)
+    bool t1_ready = false;   // ... valid: set by a fused launch, cleared by every lane reset
     int fcap = 0;
     unsigned long long* fprof = nullptr;   // BGX_FUSED_PROF: phase clocks, printed at destroy
     // harvest: records of at most L x ring (every unharvested record of every lane)
@@ -882,7 +884,7 @@ int bgx_engine_destroy(bgx_engine* e) {
         void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
                       e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records[0],
                       e->out_records[1], e->out_headers[0], e->out_headers[1], e->d_offs[0], e->d_offs[1],
-                      e->d_info[0], e->d_info[1], e->fcand, e->fvbuf, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
+                      e->d_info[0], e->d_info[1], e->fcand, e->fvbuf, e->ft1cnt, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
                       e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->dice_tab};
         for (void* p : ps) hipFree(p);
         for (hipEvent_t ev : e->ev) hipEventDestroy(ev);
@@ -981,6 +983,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             e->fcap = cfg->max_legal;
             ALLOC(e->fcand, (size_t)L * e->fcap * 8);
             ALLOC(e->fvbuf, (size_t)L * (e->fcap + 1));
+            ALLOC(e->ft1cnt, L);
         }
         if (cfg->ply == 2) {
             e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
@@ -1068,6 +1071,7 @@ int bgx_engine_set_dice(bgx_engine* e, const uint8_t* h_dice, int per_lane) {
         // every lane restarts from BackgammonEnv.reset with its scripted dice
         HIP_TRY(hipMemset(e->ctr, 0, 64));
         HIP_TRY(bgx_launch_engine_reset(&e->d, nullptr));
+        e->t1_ready = false;   // the fused launch's carried expansion belongs to the old positions
         HIP_TRY(hipDeviceSynchronize());
         return check_flags(e);
     });
@@ -1222,6 +1226,8 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     f.e = e->d;
     f.cand = e->fcand;
     f.vbuf = e->fvbuf;
+    f.t1cnt = e->ft1cnt;
+    f.t1_ready = e->t1_ready ? 1 : 0;
     f.cap = e->fcap;
     f.n_steps = n_steps;
     f.wfrag = e->net->wfrag;
@@ -1250,6 +1256,7 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     }
     if (timed(e, 0, s, true)) return BGX_E_HIP;
     HIP_TRY(bgx_launch_fused(&f, s));
+    e->t1_ready = true;   // the launch ends with every lane's next position expanded
     if (timed(e, 0, s, false)) return BGX_E_HIP;
     return BGX_OK;
 }

@@ -150,10 +150,23 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     M1.PF = P1_PF;
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int nlive = e.L - g * FL < FL ? e.L - g * FL : FL;
-        for (int v = t; v < nlive; v += NT) lane_load(e, g * FL + v, T.st[v]);
+        for (int v = t; v < nlive; v += NT) {
+            lane_load(e, g * FL + v, T.st[v]);
+            if (f.t1_ready) T.cnt[v] = f.t1cnt[g * FL + v];   // the previous launch expanded these positions
+        }
+        if (f.t1_ready) {   // the jobs' words for tier 2 (T.job), from the lane states
+            __syncthreads();
+            for (int q = t; q < nlive * 8; q += NT) {
+                const int v = q >> 3, k = q & 7;
+                const LaneState& st = T.st[v];
+                T.job[v][k] = k < 7 ? st.w[k] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
+            }
+        }
         // step s runs iff ticket(s): lockstep, s < n_steps; balanced, s < n_cap and
         // the launch's lane-step total before this workgroup-step is below the
-        // budget (thread 0 takes step s + 1's ticket before step s's queue)
+        // budget (thread 0 takes step s + 1's ticket after step s's queue, which
+        // expanded the next positions whatever the ticket says: a refused ticket
+        // ends the launch with them ready for the next one)
         auto ticket = [&](int s) -> int {
             if (f.budget <= 0) return s < f.n_steps;
             if (s >= f.n_cap) return 0;
@@ -250,7 +263,6 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             const int n_tiles = (nr + 31) >> 5;
             const int np = step >= 0 ? (nlive + 1) >> 1 : 0;   // choice items: lane pairs
             if (t == 0) {
-                T.go[(step + 1) & 1] = ticket(step + 1);
                 T.qn[0] = NW;
                 T.qn[1] = NW;
             }
@@ -258,8 +270,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             M1.map[l] = 0u;   // (tier 2 may have used the scratch)
             wave_sync();
             __syncthreads();
-            const bool nxt = T.go[(step + 1) & 1] != 0;
-            const int nj = nxt ? nlive : 0;
+            // step s + 1's tier-1 jobs (every step: the last one's results are
+            // the next launch's first; at step -1, unless the previous launch
+            // left them)
+            const int nj = step >= 0 || !f.t1_ready ? nlive : 0;
             // the next step's jobs, doubles first, when nothing runs beside them
             const bool dbl = l < nlive && T.st[l].d0 == T.st[l].d1;
             const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(l < nlive && !dbl);
@@ -443,11 +457,15 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             }
             if (prof) tw[0] += wall_clock64() - m0;
             tick(3);
+            if (t == 0) T.go[(step + 1) & 1] = ticket(step + 1);   // as late as the step allows
             __syncthreads();   // step s's lanes are stepped and step s + 1's jobs are done
             tick(4);
             if (prof && t == 0 && step >= 0) ph[5] += 1;
         }
-        for (int v = t; v < nlive; v += NT) lane_store(e, g * FL + v, T.st[v]);
+        for (int v = t; v < nlive; v += NT) {
+            lane_store(e, g * FL + v, T.st[v]);
+            f.t1cnt[g * FL + v] = T.cnt[v];   // the next positions' expansion (f.t1_ready)
+        }
         __syncthreads();
     }
     if (prof) {

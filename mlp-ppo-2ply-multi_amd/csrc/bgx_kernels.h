@@ -157,6 +157,13 @@ struct FusedArgs {
     long long budget;
     int n_cap;
     unsigned long long* budget_ctr;
+    // the next step's tier-1 results carried between launches: the last step
+    // of a launch also expands its lanes' next positions (into `cand`) and
+    // stores each lane's count (-1: tier 2) in t1cnt[lane]; t1_ready = the
+    // previous launch did so and nothing changed the lanes since (the host
+    // clears it on every reset), so the next launch starts at tier 2
+    int* t1cnt;
+    int t1_ready;
 };
 
 // TD(0) trainer (bgx_train.hip): one launch over n_eps episodes of compact
