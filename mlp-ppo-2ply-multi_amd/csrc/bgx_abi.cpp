@@ -877,6 +877,27 @@ int bgx_engine_destroy(bgx_engine* e) {
                             nd, dur[0].first, dur[nd / 2].first, mean, dur[(nd * 9) / 10].first, dur[nd - 1].first,
                             (double)(b_max - b_min) / 100.0, (double)(e_max - b_min) / 100.0, qx[28], qm[26], qm[27],
                             qx[26], qx[27]);
+                    // launch shape (median workgroup): prologue (W fragments, LUT, lane
+                    // state), the step loop, epilogue (lane state back); shader clock
+                    // over the workgroup's span (s_memtime cycles / 100 MHz wall clock)
+                    std::vector<double> pro, loop, epi, mhz;
+                    for (auto& d : dur) {
+                        const unsigned long long* q = &p[(size_t)d.second * 32];
+                        if (q[19] < q[24] || q[20] < q[19] || q[25] < q[20]) continue;
+                        pro.push_back((double)(q[19] - q[24]) / 100.0);
+                        loop.push_back((double)(q[20] - q[19]) / 100.0);
+                        epi.push_back((double)(q[25] - q[20]) / 100.0);
+                        mhz.push_back((double)q[21] / ((double)(q[25] - q[24]) / 100.0));
+                    }
+                    if (!pro.empty()) {
+                        auto med = [](std::vector<double>& v) {
+                            std::sort(v.begin(), v.end());
+                            return v[v.size() / 2];
+                        };
+                        fprintf(stderr, "[bgx fused prof] last launch shape (median workgroup): prologue %.1f us, step loop "
+                                "%.1f us, epilogue %.1f us; shader clock %.0f MHz\n", med(pro), med(loop), med(epi),
+                                med(mhz));
+                    }
                 }
             }
             hipFree(e->fprof);

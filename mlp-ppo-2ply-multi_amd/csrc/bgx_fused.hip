@@ -112,6 +112,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
 
     unsigned long long n_rows = 0, n_fb = 0, n_steps = 0;
     const unsigned long long wg_begin = PROF ? wall_clock64() : 0ull;   // this launch's span (f.prof)
+    const unsigned long long cyc_begin = PROF ? __builtin_amdgcn_s_memtime() : 0ull;   // shader clock (f.prof)
+    unsigned long long t_loop0 = 0, t_loop1 = 0;   // first step's start, last step's end (f.prof)
     // development timers (f.prof): phase sums on thread 0, per-wave sums on lane 0
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tc = 0, tw[4] = {0, 0, 0, 0}, t2c = 0, t3n = 0;
     unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
@@ -185,6 +187,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             }
         };
         const int n_iter = f.budget > 0 ? f.n_cap : f.n_steps;
+        if (prof && t == 0 && !t_loop0) t_loop0 = wall_clock64();
         // step -1 is the first step's tier-1 queue alone; step s >= 0: tier 2 and
         // the row prefix of step s, then its queue (tiles, choice pairs, step
         // s + 1's tier-1 jobs). Each item kind is issued from one place in the
@@ -462,6 +465,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             tick(4);
             if (prof && t == 0 && step >= 0) ph[5] += 1;
         }
+        if (prof && t == 0) t_loop1 = wall_clock64();
         for (int v = t; v < nlive; v += NT) {
             lane_store(e, g * FL + v, T.st[v]);
             f.t1cnt[g * FL + v] = T.cnt[v];   // the next positions' expansion (f.t1_ready)
@@ -479,6 +483,9 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             P[26] = n_rows;
             P[27] = n_fb;
             P[28] = n_steps;
+            P[19] = t_loop0;
+            P[20] = t_loop1;
+            P[21] = __builtin_amdgcn_s_memtime() - cyc_begin;
             for (int k = 0; k < 6; ++k) atomicAdd(P + k, ph[k]);
             atomicAdd(P + 11, t2c);
             atomicAdd(P + 12, n_fb);

@@ -18,6 +18,7 @@ from bgx import Engine  # noqa: E402
 d = np.load(os.path.join(REPO, "tests", "golden", "weights_seed0.npz"))
 w = {k: d[k] for k in ("W1", "b1", "w2", "b2")}
 steps = int(os.environ.get("STEPS", "20"))
+sleep_s = float(os.environ.get("SLEEP_MS", "20")) / 1e3   # idle gap before each window
 torch.cuda.set_device(0)
 e = Engine(lanes=8192, seed=0, balance=True)
 e.set_weights(w, 1.5, 1)
@@ -27,7 +28,8 @@ for _ in range(3):
 e.sync()
 out = []
 for i in range(10):
-    time.sleep(0.02)
+    if sleep_s > 0:
+        time.sleep(sleep_s)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e.step(steps)
@@ -36,6 +38,6 @@ for i in range(10):
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     out.append({"us": (t1 - t0) * 1e6, "episodes": h.n_episodes, "records": h.n_records})
-print(json.dumps({"steps": steps, "windows": out,
+print(json.dumps({"steps": steps, "sleep_ms": sleep_s * 1e3, "windows": out,
                   "median_us": float(np.median([o["us"] for o in out]))}))
 e.close()
