@@ -162,15 +162,24 @@ struct bgx_engine {
     int fcap = 0;
     unsigned long long* fprof = nullptr;   // BGX_FUSED_PROF: phase clocks, printed at destroy
     // harvest: records of at most L x ring (every unharvested record of every lane)
-    // two harvest buffers (bgx_harvest_enqueue / _fetch): ticket t uses slot t & 1
-    uint32_t* out_records[2] = {nullptr, nullptr};
-    uint32_t* out_headers[2] = {nullptr, nullptr};   // [ep_cap][16] copies of the finished episodes' headers
-    int32_t* d_offs[2] = {nullptr, nullptr};     // [ep_cap + 1]
-    uint32_t* d_info[2] = {nullptr, nullptr};    // [4] harvest_scan_kernel totals
-    uint32_t* h_info = nullptr;    // [2][4] host-mapped copies, written by harvest_scan_kernel itself
+    // three harvest buffers (bgx_harvest_enqueue / _fetch): ticket t uses slot
+    // t % 3. A ticket's arrays live until the second harvest after it; the
+    // fused engine harvests inside its launches, so the launches between
+    // tickets t + 1 and t + 2 already fill slot (t + 2) % 3: a third slot keeps
+    // ticket t's arrays intact until then
+    static constexpr int NHB = 3;
+    uint32_t* out_records[NHB] = {nullptr, nullptr, nullptr};
+    uint32_t* out_headers[NHB] = {nullptr, nullptr, nullptr};   // [ep_cap][16] copies of the finished episodes' headers
+    int32_t* d_offs[NHB] = {nullptr, nullptr, nullptr};     // [ep_cap + 1]
+    uint32_t* d_info[NHB] = {nullptr, nullptr, nullptr};    // [4] harvest totals
+    uint32_t* h_info = nullptr;    // [NHB][4] host-mapped copies, written by the harvesting kernel itself
     uint32_t* h_info_dev = nullptr;   // its device address
+    // fused engine (in-kernel harvest): per slot the running {episodes << 32 |
+    // records} appended since the previous ticket, [NHB] = finished workgroups
+    unsigned long long* fh_ctr = nullptr;
+    bool fh_launched = false;      // a fused launch filled the current slot since the last ticket
     hipEvent_t hev = nullptr;         // the engine's last step, for a harvest on another stream
-    hipEvent_t hdone[2] = {nullptr, nullptr};   // a slot's harvest kernels finished
+    hipEvent_t hdone[NHB] = {nullptr, nullptr, nullptr};   // a slot's harvest finished
     hipStream_t hstream = nullptr;    // stream of the last enqueued harvest (the next step waits for it)
     int h_tickets = 0;                // harvests enqueued so far
     // timing
@@ -904,7 +913,8 @@ int bgx_engine_destroy(bgx_engine* e) {
         }
         void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
                       e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records[0],
-                      e->out_records[1], e->out_headers[0], e->out_headers[1], e->d_offs[0], e->d_offs[1],
+                      e->out_records[1], e->out_records[2], e->out_headers[0], e->out_headers[1], e->out_headers[2],
+                      e->d_offs[0], e->d_offs[1], e->d_offs[2], e->d_info[2], e->fh_ctr, e->d.hring, e->d.hepi,
                       e->d_info[0], e->d_info[1], e->fcand, e->fvbuf, e->ft1cnt, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
                       e->d.rec_count, e->d.ep_first, e->d.harv, e->d.ring, e->d.ep_list, e->dice_tab};
         for (void* p : ps) hipFree(p);
@@ -982,7 +992,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         ALLOC(d.harv, L);
         ALLOC(d.ring, (size_t)L * ring * bgx::REC_WORDS);
         ALLOC(d.ep_list, (size_t)ep_cap * bgx::EP_WORDS);
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < bgx_engine::NHB; ++b) {
             ALLOC(e->out_records[b], (size_t)L * ring * bgx::REC_WORDS);
             ALLOC(e->out_headers[b], (size_t)ep_cap * bgx::EP_WORDS);
             ALLOC(e->d_offs[b], (size_t)ep_cap + 1);
@@ -990,7 +1000,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             if (!rc && hipEventCreateWithFlags(&e->hdone[b], hipEventDisableTiming) != hipSuccess)
                 rc = fail(BGX_E_HIP, "hipEventCreate failed");
         }
-        if (!rc && (hipHostMalloc((void**)&e->h_info, 8 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+        if (!rc && (hipHostMalloc((void**)&e->h_info, 4 * bgx_engine::NHB * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
                         hipSuccess ||
                     hipHostGetDevicePointer((void**)&e->h_info_dev, e->h_info, 0) != hipSuccess))
             rc = fail(BGX_E_HIP, "hipHostMalloc (mapped) failed");
@@ -1005,6 +1015,14 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             ALLOC(e->fcand, (size_t)L * e->fcap * 8);
             ALLOC(e->fvbuf, (size_t)L * (e->fcap + 1));
             ALLOC(e->ft1cnt, L);
+            // per-lane episode headers for the in-kernel harvest: at most
+            // (ring - max_steps) / 13 + 1 episodes finish between two harvests
+            int hr = 1;
+            while (hr < (ring - cfg->max_steps) / kMinGameSteps + 2) hr <<= 1;
+            d.HR = hr;
+            ALLOC(d.hring, (size_t)L * hr * bgx::EP_WORDS);
+            ALLOC(d.hepi, L);
+            ALLOC(e->fh_ctr, bgx_engine::NHB + 1);
         }
         if (cfg->ply == 2) {
             e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
@@ -1026,7 +1044,8 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             bgx_engine_destroy(e);
             return rc;
         }
-        if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess) {
+        if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess ||
+            (e->fh_ctr && hipMemset(e->fh_ctr, 0, (bgx_engine::NHB + 1) * sizeof(unsigned long long)) != hipSuccess)) {
             bgx_engine_destroy(e);
             return fail(BGX_E_HIP, "hipMemset failed");
         }
@@ -1268,6 +1287,17 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
         f.n_cap = cap < headroom ? cap : headroom;
         f.budget_ctr = (unsigned long long*)(e->ctr + C_BUDGET);
     }
+    {   // in-kernel harvest into the slot of the next ticket
+        const int b = e->h_tickets % bgx_engine::NHB;
+        f.hv_hdr = e->out_headers[b];
+        f.hv_rec = e->out_records[b];
+        f.hv_ep_cap = e->d.ep_cap;
+        f.hv_ctr = e->fh_ctr + b;
+        f.hv_next = e->fh_ctr + (b + 1) % bgx_engine::NHB;
+        f.hv_info = e->d_info[b];
+        f.hv_hinfo = e->h_info_dev + 4 * b;
+        f.done_ctr = e->fh_ctr + bgx_engine::NHB;
+    }
     if (e->prof_enabled) {
         if (!e->fprof) {
             if (dalloc(&e->fprof, (size_t)1024 * 32)) return BGX_E_HIP;
@@ -1278,6 +1308,7 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     if (timed(e, 0, s, true)) return BGX_E_HIP;
     HIP_TRY(bgx_launch_fused(&f, s));
     e->t1_ready = true;   // the launch ends with every lane's next position expanded
+    e->fh_launched = true;
     if (timed(e, 0, s, false)) return BGX_E_HIP;
     return BGX_OK;
 }
@@ -1294,7 +1325,7 @@ int bgx_step(bgx_engine* e, int n_steps, void* stream) {
         // an enqueued harvest on another stream reads the rings and resets the
         // episode list: the step waits for it (an event, no host wait)
         if (e->h_tickets > 0 && e->hstream != s)
-            HIP_TRY(hipStreamWaitEvent(s, e->hdone[(e->h_tickets - 1) & 1], 0));
+            HIP_TRY(hipStreamWaitEvent(s, e->hdone[(e->h_tickets - 1) % bgx_engine::NHB], 0));
         e->last = s;
         if (n_steps == 0) return BGX_OK;
         // timed runs launch directly (events between the kernels); otherwise the
@@ -1347,14 +1378,23 @@ int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream) {
             HIP_TRY(hipEventRecord(e->hev, e->last));
             HIP_TRY(hipStreamWaitEvent(s, e->hev, 0));
         }
-        const int t = e->h_tickets, b = t & 1;
+        const int t = e->h_tickets, b = t % bgx_engine::NHB;
         // offsets and totals on the device (harvest_scan_kernel, which also writes
         // {episodes, records, error flags} into host-mapped memory), then the copy
         // of the finished episodes' headers and records (a persistent grid that
         // reads the episode count on the device: no host round trip in between)
-        HIP_TRY(bgx_launch_harvest_scan(&e->d, e->d_offs[b], e->d_info[b], e->h_info_dev + 4 * b, s));
-        HIP_TRY(bgx_launch_harvest_gather(&e->d, e->d_offs[b], e->d_info[b], e->out_headers[b], e->out_records[b],
-                                          s));
+        if (e->fused) {
+            // the fused launches since the last ticket harvested into slot b and
+            // published its totals; with none, publish the (empty) slot here
+            if (!e->fh_launched)
+                HIP_TRY(bgx_launch_harvest_close(e->fh_ctr + b, e->fh_ctr + (b + 1) % bgx_engine::NHB, e->ctr + C_ERR,
+                                                 e->d_info[b], e->h_info_dev + 4 * b, s));
+            e->fh_launched = false;
+        } else {
+            HIP_TRY(bgx_launch_harvest_scan(&e->d, e->d_offs[b], e->d_info[b], e->h_info_dev + 4 * b, s));
+            HIP_TRY(bgx_launch_harvest_gather(&e->d, e->d_offs[b], e->d_info[b], e->out_headers[b], e->out_records[b],
+                                              s));
+        }
         HIP_TRY(hipEventRecord(e->hdone[b], s));
         e->hstream = s;
         e->h_tickets = t + 1;
@@ -1370,7 +1410,7 @@ int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out) {
             return fail(BGX_E_ARG, "bgx_harvest_fetch: ticket %d is not one of the last two harvests (%d enqueued)",
                         ticket, e->h_tickets);
         HIP_TRY(hipSetDevice(e->device));
-        const int b = ticket & 1;
+        const int b = ticket % bgx_engine::NHB;
         HIP_TRY(hipEventSynchronize(e->hdone[b]));
         const uint32_t* info = e->h_info + 4 * b;
         const uint32_t flags = info[2];

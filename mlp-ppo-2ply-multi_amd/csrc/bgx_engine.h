@@ -176,7 +176,7 @@ BGX_DEV Outcome judge(const uint32_t* w, int pl, uint32_t& flags) {
 struct LaneState {
     uint32_t w[8];        // board, indicator flag = player to move
     int p, d0, d1, steps;
-    uint32_t flags, epi, rec, ep_first, harv;
+    uint32_t flags, epi, rec, ep_first, harv, hepi;
     uint64_t ctr;         // Philox counter
 };
 BGX_DEV void lane_load(const EngineDev& e, int i, LaneState& s) {
@@ -190,6 +190,7 @@ BGX_DEV void lane_load(const EngineDev& e, int i, LaneState& s) {
     s.rec = e.rec_count[i];
     s.ep_first = e.ep_first[i];
     s.harv = e.harv[i];
+    s.hepi = e.hepi ? e.hepi[i] : 0u;
     s.ctr = e.rng[i];
 }
 // everything but the board row (lane_advance writes that every step)
@@ -269,9 +270,16 @@ BGX_DEV void lane_advance(const EngineDev& e, int i, LaneState& s, Rng& rng, int
     set_flag(s.w, s.p);
     if (done || s.steps >= e.max_steps) {
         if (lead) {
-            const uint32_t slot = atomicAdd(e.ep_count, 1u);
-            if ((int)slot < e.ep_cap) {
-                uint32_t* h = e.ep_list + (size_t)slot * EP_WORDS;
+            // the header: the lane's own ring (fused engine: its workgroup
+            // harvests it) or the engine's episode list
+            uint32_t* h = nullptr;
+            if (e.hring) {
+                if (s.epi - s.hepi < (uint32_t)e.HR) h = e.hring + ((size_t)i * e.HR + (s.epi & (uint32_t)(e.HR - 1))) * EP_WORDS;
+            } else {
+                const uint32_t slot = atomicAdd(e.ep_count, 1u);
+                if ((int)slot < e.ep_cap) h = e.ep_list + (size_t)slot * EP_WORDS;
+            }
+            if (h) {
                 const uint32_t first = s.ep_first, nrec = s.rec - first;
                 ((uint4*)h)[0] = make_uint4((uint32_t)(e.lane_base + i), s.epi, first, nrec);
                 ((uint4*)h)[1] = make_uint4((uint32_t)s.steps,

@@ -40,6 +40,7 @@ __global__ __launch_bounds__(256) void engine_reset_kernel(EngineDev e) {
     e.rec_count[i] = 0;
     e.ep_first[i] = 0;
     e.harv[i] = 0;
+    if (e.hepi) e.hepi[i] = 0;
 }
 
 
@@ -382,7 +383,28 @@ __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t
     }
 }
 
+// in-kernel harvest (fused engine) with no fused launch since the last ticket:
+// the ticket's totals are whatever its counter holds (nothing was appended)
+__global__ void harvest_close_kernel(unsigned long long* ctr, unsigned long long* next, const unsigned* err_flags,
+                                     uint32_t* info, uint32_t* hinfo) {
+    const unsigned long long c = *ctr;
+    const uint32_t v[4] = {(uint32_t)(c >> 32), (uint32_t)c, *err_flags, (uint32_t)(c >> 32)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        info[k] = v[k];
+        if (hinfo) hinfo[k] = v[k];
+    }
+    *next = 0ull;
+}
+
 }  // namespace bgx
+
+extern "C" hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next,
+                                               const unsigned* err_flags, uint32_t* info, uint32_t* hinfo,
+                                               hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::harvest_close_kernel, dim3(1), dim3(1), 0, stream, ctr, next, err_flags, info, hinfo);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t bgx_launch_engine_reset(const bgx::EngineDev* e, hipStream_t stream) {
     hipLaunchKernelGGL(bgx::engine_reset_kernel, dim3((e->L + 255) / 256), dim3(256), 0, stream, *e);

@@ -94,8 +94,13 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     for (int i = t; i < 64; i += NT) T.tdone[i] = 0u;
     for (int i = t; i < FL; i += NT) T.chosen[i] = T.claim[i] = 0u;
     unsigned qtag = 0u;   // this workgroup's step counter (tags the flags; never 0 on a live step)
-    uint4* wl = (uint4*)(lds + F_W);     // split-fp16 W fragments, loaded once
-    for (int k = t; k < NFRAG; k += NT) wl[k] = f.wfrag[k];
+    // split-fp16 W fragments, loaded once, global -> LDS by LDS-DMA (every load
+    // of a wave in flight at once; the prologue's lane loads overlap them)
+    uint4* wl = (uint4*)(lds + F_W);
+    static_assert(NFRAG % 64 == 0, "W fragments in whole wave chunks");
+    for (int c = w; c < NFRAG / 64; c += NW)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(void*)(f.wfrag + 64 * c + l),
+                                         (__attribute__((address_space(3))) void*)(void*)(wl + 64 * c), 16, 0, 0);
     const uint4* wf = wl;
 
     MovegenArgs a{};
@@ -150,6 +155,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     M1.pa = slw + 64;
     M1.pb = M1.pa + P1_PF;
     M1.PF = P1_PF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's W fragment loads landed (a barrier follows)
     for (int g = (int)blockIdx.x; g < groups; g += (int)gridDim.x) {
         const int nlive = e.L - g * FL < FL ? e.L - g * FL : FL;
         for (int v = t; v < nlive; v += NT) {
@@ -470,6 +476,69 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             lane_store(e, g * FL + v, T.st[v]);
             f.t1cnt[g * FL + v] = T.cnt[v];   // the next positions' expansion (f.t1_ready)
         }
+        if (f.hv_hdr) {
+            // ---- in-kernel harvest: this group's finished episodes (headers from
+            // the lanes' header rings, records from their record rings) appended to
+            // the ticket's output at offsets from one 64-bit atomic, while other
+            // workgroups still run their last steps (the scratch is free here)
+            uint32_t* hs = (uint32_t*)lds;   // [0, 64) episode prefix, [64, 128) record prefix, [128, 132) totals
+            if (w == 0) {
+                int ne = 0, nr = 0;
+                if (l < nlive) {
+                    const LaneState& s = T.st[l];
+                    ne = (int)(s.epi - s.hepi);
+                    nr = (int)(s.ep_first - s.harv);
+                }
+                const int ie = wave_incl_scan(ne), ir = wave_incl_scan(nr);
+                const uint32_t te = (uint32_t)__shfl(ie, 63), tr = (uint32_t)__shfl(ir, 63);
+                if (l < FL) {
+                    hs[l] = (uint32_t)(ie - ne);
+                    hs[64 + l] = (uint32_t)(ir - nr);
+                }
+                if (l == 0) {
+                    const unsigned long long base =
+                        te | tr ? atomicAdd(f.hv_ctr, ((unsigned long long)te << 32) | tr) : 0ull;
+                    hs[128] = te;
+                    hs[129] = tr;
+                    hs[130] = (uint32_t)(base >> 32);
+                    hs[131] = (uint32_t)base;
+                }
+            }
+            __syncthreads();
+            const uint32_t te = hs[128], tr = hs[129], be = hs[130], br = hs[131];
+            // lane of the k-th episode / record: the last v with prefix[v] <= k
+            auto owner = [&](const uint32_t* pre, uint32_t k) -> int {
+                int v = 0;
+#pragma unroll
+                for (int sstep = FL / 2; sstep >= 1; sstep >>= 1)
+                    if (pre[v + sstep] <= k) v += sstep;
+                return v;
+            };
+            if (be + te <= (uint32_t)f.hv_ep_cap) {
+                for (uint32_t q = (uint32_t)t; q < 4u * te; q += NT) {   // 4 x uint4 per header
+                    const uint32_t k = q >> 2;
+                    const int v = owner(hs, k);
+                    const uint32_t ep = T.st[v].hepi + (k - hs[v]);
+                    const uint4* src = (const uint4*)(e.hring + ((size_t)(g * FL + v) * e.HR + (ep & (uint32_t)(e.HR - 1))) *
+                                                                    EP_WORDS);
+                    ((uint4*)(f.hv_hdr + (size_t)(be + k) * EP_WORDS))[q & 3u] = src[q & 3u];
+                }
+                for (uint32_t q = (uint32_t)t; q < 3u * tr; q += NT) {   // 3 x uint4 per record
+                    const uint32_t r = q / 3u, c = q - 3u * r;
+                    const int v = owner(hs + 64, r);
+                    const uint32_t rr = T.st[v].harv + (r - hs[64 + v]);
+                    const uint4* src =
+                        (const uint4*)(e.ring + ((size_t)(g * FL + v) * e.R + (rr & (uint32_t)(e.R - 1))) * REC_WORDS);
+                    ((uint4*)(f.hv_rec + (size_t)(br + r) * REC_WORDS))[c] = src[c];
+                }
+            } else if (t == 0) {
+                atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
+            }
+            for (int v = t; v < nlive; v += NT) {
+                e.harv[g * FL + v] = T.st[v].ep_first;
+                e.hepi[g * FL + v] = T.st[v].epi;
+            }
+        }
         __syncthreads();
     }
     if (prof) {
@@ -503,13 +572,26 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         atomicAdd(e.stats + 3, n_rows);
         atomicAdd(e.stats + 4, n_steps);
         atomicAdd(e.stats + 5, n_fb);
-        if (f.budget > 0) {
+        if (f.budget > 0 || f.hv_hdr) {
             // the last workgroup to finish zeroes the lane-step counter for the
-            // next launch (stream order: no memset launch in between)
+            // next launch and publishes the harvest totals (stream order: no
+            // memset or harvest launch in between)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            if (atomicAdd(f.budget_ctr + 1, 1ull) == (unsigned long long)gridDim.x - 1ull) {
-                __hip_atomic_store(f.budget_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(f.budget_ctr + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (atomicAdd(f.done_ctr, 1ull) == (unsigned long long)gridDim.x - 1ull) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (f.budget > 0) __hip_atomic_store(f.budget_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (f.hv_hdr) {
+                    const unsigned long long c = __hip_atomic_load(f.hv_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t fl = __hip_atomic_load(e.err_flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t v[4] = {(uint32_t)(c >> 32), (uint32_t)c, fl, (uint32_t)(c >> 32)};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        f.hv_info[k] = v[k];
+                        if (f.hv_hinfo) f.hv_hinfo[k] = v[k];   // host-mapped (vector stores)
+                    }
+                    __hip_atomic_store(f.hv_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __hip_atomic_store(f.done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }

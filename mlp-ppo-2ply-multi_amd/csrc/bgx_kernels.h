@@ -112,6 +112,12 @@ struct EngineDev {
     uint32_t* ep_list;           // [ep_cap][EP_WORDS]
     unsigned* ep_count;
     int ep_cap;
+    // fused engine: finished-episode headers go to a per-lane ring instead of
+    // ep_list, so a fused workgroup harvests its own lanes at the end of a
+    // launch (FusedArgs hv_*); null on the phased engines
+    uint32_t* hring;             // [L][HR][EP_WORDS], slot = episode number & (HR - 1)
+    int HR;                      // header slots per lane (a power of two)
+    uint32_t* hepi;              // [L] episodes harvested (absolute episode number)
     // per-step inputs
     const int32_t* cand_off;     // [L] offset of the lane's candidates after row L
     const int32_t* cand_cnt;     // [L] full candidate count
@@ -151,8 +157,8 @@ struct FusedArgs {
     // balanced launch (bgx_config.balance): each workgroup-step takes a ticket of
     // its lanes from budget_ctr[0] and steps while the running total is below
     // `budget` lane-steps, at most n_cap steps; budget <= 0: every lane runs
-    // exactly n_steps (lockstep). budget_ctr[1] counts finished workgroups; the
-    // last one zeroes both (budget_ctr is zero at engine create). The launcher
+    // exactly n_steps (lockstep). The last workgroup to finish (done_ctr) zeroes
+    // budget_ctr (zero at engine create) for the next launch. The launcher
     // balances only when each workgroup owns one lane group.
     long long budget;
     int n_cap;
@@ -164,6 +170,21 @@ struct FusedArgs {
     // clears it on every reset), so the next launch starts at tier 2
     int* t1cnt;
     int t1_ready;
+    // in-kernel harvest (fused engine): each workgroup, once its lanes are done
+    // for the launch, appends their finished episodes (headers from e.hring,
+    // records from the lane rings) to this ticket's output at offsets from one
+    // 64-bit atomic (episodes << 32 | records) and sets the lanes' harvested
+    // marks; the last workgroup to finish publishes the totals {episodes,
+    // records, error flags, episodes} to hv_info / hv_hinfo and zeroes the next
+    // output's counter. hv_hdr null: no harvest in this launch.
+    uint32_t* hv_hdr;            // [ep cap][EP_WORDS]
+    uint32_t* hv_rec;            // [L * R][REC_WORDS]
+    int hv_ep_cap;
+    unsigned long long* hv_ctr;  // this output's running totals
+    unsigned long long* hv_next; // the next output's (zeroed by the last workgroup)
+    uint32_t* hv_info;           // [4] device
+    uint32_t* hv_hinfo;          // [4] host-mapped
+    unsigned long long* done_ctr;   // finished workgroups of the launch (the last one zeroes it)
 };
 
 // TD(0) trainer (bgx_train.hip): one launch over n_eps episodes of compact
@@ -210,6 +231,10 @@ hipError_t bgx_launch_td0(const bgx::TrainArgs* args, hipStream_t stream);
 // count is read on the device)
 hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* hinfo,
                                    hipStream_t stream);
+// in-kernel harvest bookkeeping when no fused launch ran since the last ticket:
+// publish the (empty) totals of ctr and zero the next output's counter
+hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next, const unsigned* err_flags,
+                                    uint32_t* info, uint32_t* hinfo, hipStream_t stream);
 hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
                                      uint32_t* hout, uint32_t* out, hipStream_t stream);
 }

@@ -422,6 +422,50 @@ def test_fused_balanced_launch_keeps_every_lane_game(weights_seed0, fl, monkeypa
             np.testing.assert_array_equal(a[key][1][f], b[key][1][f], err_msg=f"{key} {f}")
 
 
+def test_fused_in_kernel_harvest_slots(weights_seed0):
+    """The fused engine harvests inside its launches (each workgroup appends
+    its own lanes' finished episodes at the end of a launch, bgx_fused.hip):
+    two launches between tickets accumulate into one harvest, a ticket with no
+    launch since the previous one is empty, and a ticket's arrays stay intact
+    until the second harvest_enqueue after it although the launches after the
+    next ticket already harvest (three slots). The episodes equal the phased
+    engine's (which harvests with its own kernels) record for record."""
+    from bgx.episodes import decode_records
+    ref = _engine(weights_seed0, lanes=96, seed=31, ply=1, fused=False)
+    want = _by_episode(*_collect(ref, 200, chunk=40))
+    ref.close()
+    e = _engine(weights_seed0, lanes=96, seed=31, ply=1, fused=True)
+    hdrs, recs = [], []
+
+    def take(t):
+        h = e.harvest_fetch(t)
+        hdr = h.headers.cpu().numpy().view(np.uint32)
+        hdrs.append(hdr)
+        recs.append(decode_records(hdr, h.records))
+        return hdr.shape[0]
+
+    e.step(40)
+    e.step(40)                  # two launches, one harvest
+    t0 = e.harvest_enqueue()
+    t1 = e.harvest_enqueue()    # nothing ran since t0
+    e.step(40)                  # harvests into t2's slot while t0 / t1 are unread
+    assert take(t0) > 0
+    assert take(t1) == 0
+    t2 = e.harvest_enqueue()
+    e.step(40)                  # t3's slot
+    t3 = e.harvest_enqueue()
+    e.step(40)                  # t4's slot = t1's: t2 and t3 must still be intact
+    assert take(t2) > 0 and take(t3) > 0
+    take(e.harvest_enqueue())
+    e.close()
+    got = _by_episode(hdrs, recs)
+    assert len(got) > 50 and got.keys() == want.keys()
+    for key in want:
+        np.testing.assert_array_equal(got[key][0], want[key][0], err_msg=str(key))
+        for f in want[key][1]:
+            np.testing.assert_array_equal(got[key][1][f], want[key][1][f], err_msg=f"{key} {f}")
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_pipelined_harvest_equals_synchronous(weights_seed0, fused):
     """harvest_enqueue / harvest_fetch (the next step queued before the host
