@@ -220,6 +220,9 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     return el, d, tm, d_tm, gathered
 
 
+CPU_WARMUP_STEPS = 300   # BASELINE.md's CPU plan: a 300-step warm-up, then the timed window
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -245,15 +248,18 @@ def _cpu_worker(core, tasks, results):
         t = tasks.get()
         if t is None:
             return
-        seed, ply, seconds = t
-        results.put(orc.selfplay_bench(w, temperature=1.5, seed=seed, n_threads=1, seconds=seconds, ply=ply))
+        seed, ply, seconds, warmup = t
+        results.put(orc.selfplay_bench(w, temperature=1.5, seed=seed, n_threads=1, seconds=seconds, ply=ply,
+                                       warmup=warmup))
 
 
 def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
     """The CPU port of the worker loop (oracle/bgref.c, pinned by the golden
     fixtures) as `procs` processes, each pinned to its own host core: one
-    1-ply round per seed (median of the per-round aggregates), then one 2-ply
-    K=4 round. Runs before this process touches the GPU."""
+    1-ply round per seed, each process timing its window after a 300-step
+    warm-up of whole games (BASELINE.md's plan; median of the per-round
+    aggregates), then one 2-ply K=4 round (no warm-up: at ~30 decisions/s per
+    core it would take ten seconds). Runs before this process touches the GPU."""
     import multiprocessing as mp
     cores = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
     ctx = mp.get_context("spawn")
@@ -264,9 +270,9 @@ def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
     for w in ws:
         w.start()
 
-    def round_(seed, ply, seconds):
+    def round_(seed, ply, seconds, warmup=0):
         for i in range(procs):
-            tasks[i].put((1000 * seed + i, ply, seconds))
+            tasks[i].put((1000 * seed + i, ply, seconds, warmup))
         rs = [results.get(timeout=600) for _ in range(procs)]
         return rs, max(r["elapsed"] for r in rs)
 
@@ -274,7 +280,7 @@ def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
     try:
         rates = []
         for s in seeds:
-            rs, el = round_(s, 1, seconds_1ply)
+            rs, el = round_(s, 1, seconds_1ply, warmup=CPU_WARMUP_STEPS)
             rates.append(sum(r["steps"] for r in rs) / el)
         out["1ply"] = {"rates": rates, "median": float(np.median(rates))}
         if seconds_2ply > 0:
@@ -448,7 +454,7 @@ def main():
         r = cpu_baseline(args.cpu_procs, args.cpu_seconds, list(range(args.cpu_seeds)), args.cpu_2ply_seconds)
         cpu = {"value": r["1ply"]["median"], "unit": "env_steps/s", "cores": r["cores_used"], "kind": "port",
                "sample": (f"{args.cpu_procs} processes, each pinned to one host core, x {args.cpu_seconds:.0f} s "
-                          f"of 1-ply self-play per seed (seeds 0-{args.cpu_seeds - 1}, median of "
+                          f"of 1-ply self-play per seed after a {CPU_WARMUP_STEPS}-step warm-up (seeds 0-{args.cpu_seeds - 1}, median of "
                           f"{[round(x) for x in r['1ply']['rates']]}) with the CPU port of the worker loop "
                           f"(oracle/bgref.c; same weights, T=1.5); host: {r['cpu_model']}, nproc {r['nproc']}, "
                           f"{r['affinity']} cores in this process's affinity mask; the reference's own Python "

@@ -673,6 +673,8 @@ typedef struct {
     long long steps, decisions, episodes;
     int ply;          /* 1: softmax(V/T) over every candidate (worker.py:137-143);
                          2: two_ply.py:44-90 scoring of the top-4 by V, softmax over the four */
+    long long warmup; /* untimed env steps first (whole games, BASELINE.md: a 300-step warm-up) */
+    double elapsed;   /* the thread's timed window */
 } sp_arg;
 
 /* compute_weighted_opponent_response (two_ply.py:93-150), exact mode, in
@@ -745,7 +747,8 @@ static void* sp_thread(void* p) {
     float* v2 = (float*)malloc(sizeof(float) * 500);
     double t0 = now_s();
     long long steps = 0, dec = 0, eps = 0;
-    while (now_s() - t0 < a->seconds) {
+    int warm = a->warmup > 0;
+    while (warm || now_s() - t0 < a->seconds) {
         /* reset (backgammon_env.py:92-128) */
         uint8_t board[52], roll[2];
         memcpy(board, INITIAL, 52);
@@ -812,7 +815,13 @@ static void* sp_thread(void* p) {
         }
         steps += step;
         ++eps;
+        if (warm && steps >= a->warmup) {   /* the warm-up ends at a game boundary: start the clock */
+            warm = 0;
+            steps = dec = eps = 0;
+            t0 = now_s();
+        }
     }
+    a->elapsed = now_s() - t0;
     a->steps = steps;
     a->decisions = dec;
     a->episodes = eps;
@@ -832,20 +841,29 @@ long long bgref_selfplay_bench_ply(const float* W1, const float* b1, const float
                                    const float* b2, float temperature, uint64_t seed,
                                    int n_threads, double seconds, int ply, long long* decisions,
                                    long long* episodes, double* elapsed) {
+    return bgref_selfplay_bench_warm(W1, b1, w2, b2, temperature, seed, n_threads, seconds, ply, 0,
+                                     decisions, episodes, elapsed);
+}
+
+long long bgref_selfplay_bench_warm(const float* W1, const float* b1, const float* w2,
+                                    const float* b2, float temperature, uint64_t seed,
+                                    int n_threads, double seconds, int ply, long long warmup,
+                                    long long* decisions, long long* episodes, double* elapsed) {
     if (n_threads < 1) n_threads = 1;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * n_threads);
     sp_arg* args = (sp_arg*)calloc(n_threads, sizeof(sp_arg));
-    double t0 = now_s();
     for (int i = 0; i < n_threads; ++i) {
-        args[i] = (sp_arg){W1, b1, w2, b2, temperature, seed, i, seconds, 0, 0, 0, ply};
+        args[i] = (sp_arg){W1, b1, w2, b2, temperature, seed, i, seconds, 0, 0, 0, ply, warmup, 0.0};
         pthread_create(&th[i], NULL, sp_thread, &args[i]);
     }
     long long s = 0, d = 0, e = 0;
+    double el = 0.0;   /* the longest thread window (each starts after its own warm-up) */
     for (int i = 0; i < n_threads; ++i) {
         pthread_join(th[i], NULL);
         s += args[i].steps; d += args[i].decisions; e += args[i].episodes;
+        if (args[i].elapsed > el) el = args[i].elapsed;
     }
-    if (elapsed) *elapsed = now_s() - t0;
+    if (elapsed) *elapsed = el;
     if (decisions) *decisions = d;
     if (episodes) *episodes = e;
     free(th); free(args);

@@ -128,6 +128,13 @@ long long bgref_selfplay_bench_ply(const float* W1, const float* b1, const float
                                    int n_threads, double seconds, int ply,
                                    long long* decisions, long long* episodes,
                                    double* elapsed);
+/* the same with `warmup` untimed env steps per thread first (whole games;
+   BASELINE.md's CPU plan: a 300-step warm-up, then the timed window) */
+long long bgref_selfplay_bench_warm(const float* W1, const float* b1, const float* w2,
+                                    const float* b2, float temperature, uint64_t seed,
+                                    int n_threads, double seconds, int ply, long long warmup,
+                                    long long* decisions, long long* episodes,
+                                    double* elapsed);
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,12 @@ def lib():
                                                ctypes.c_int, ctypes.POINTER(ctypes.c_longlong),
                                                ctypes.POINTER(ctypes.c_longlong), f64p]
         L.bgref_selfplay_bench_ply.restype = ctypes.c_longlong
+        L.bgref_selfplay_bench_warm.argtypes = [f32p, f32p, f32p, f32p, ctypes.c_float,
+                                                ctypes.c_uint64, ctypes.c_int, ctypes.c_double,
+                                                ctypes.c_int, ctypes.c_longlong,
+                                                ctypes.POINTER(ctypes.c_longlong),
+                                                ctypes.POINTER(ctypes.c_longlong), f64p]
+        L.bgref_selfplay_bench_warm.restype = ctypes.c_longlong
         _lib = L
     return _lib
 
@@ -200,15 +206,15 @@ def philox(key, ctr_hi, ctr_lo):
     return list(out)
 
 
-def selfplay_bench(weights, temperature=1.5, seed=0, n_threads=1, seconds=5.0, ply=1):
+def selfplay_bench(weights, temperature=1.5, seed=0, n_threads=1, seconds=5.0, ply=1, warmup=0):
     W1, b1, w2, b2 = (np.ascontiguousarray(weights[k], dtype=np.float32)
                       for k in ("W1", "b1", "w2", "b2"))
     dec = ctypes.c_longlong(0)
     eps = ctypes.c_longlong(0)
     el = ctypes.c_double(0)
-    steps = lib().bgref_selfplay_bench_ply(_f32(W1), _f32(b1), _f32(w2), _f32(b2),
-                                           float(temperature), int(seed), int(n_threads),
-                                           float(seconds), int(ply), ctypes.byref(dec),
-                                           ctypes.byref(eps), ctypes.byref(el))
+    steps = lib().bgref_selfplay_bench_warm(_f32(W1), _f32(b1), _f32(w2), _f32(b2),
+                                            float(temperature), int(seed), int(n_threads),
+                                            float(seconds), int(ply), int(warmup), ctypes.byref(dec),
+                                            ctypes.byref(eps), ctypes.byref(el))
     return {"steps": int(steps), "decisions": int(dec.value), "episodes": int(eps.value),
             "elapsed": float(el.value), "threads": int(n_threads)}
