@@ -209,9 +209,12 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream);
  * steps: bgx_harvest_enqueue queues the harvest on `stream` (behind the
  * engine's last step; the next bgx_step waits for it) and returns a ticket at
  * once; bgx_harvest_fetch(ticket) waits for that harvest and fills `out` as
- * bgx_harvest does. Two buffers alternate: a ticket's arrays stay valid until
+ * bgx_harvest does. Three buffers rotate: a ticket's arrays stay valid until
  * the second bgx_harvest_enqueue after it, and only the last two tickets can
- * be fetched. (bgx_harvest = enqueue + fetch.) */
+ * be fetched. (bgx_harvest = enqueue + fetch.) A fused 1-ply engine harvests
+ * inside its step launches (each workgroup its own lanes, into the buffer of
+ * the next ticket), so enqueue only records the point; the contract is the
+ * same. */
 int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream);
 int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out);
 
