@@ -231,6 +231,18 @@ def make_tag() -> str:
     return f"{os.getpid()}_{secrets.token_hex(4)}"
 
 
+def shm_fits(world: int, slot_bytes: int, path: str = "/dev/shm", margin: float = 1.25) -> bool:
+    """Whether the node's shared-memory filesystem has room for every rank's
+    segment (a header + two slots each, page-locked in full). A tmpfs accepts
+    a larger segment at creation and fails only when its pages are touched,
+    so the launcher checks first and otherwise uses the RCCL gather."""
+    try:
+        st = os.statvfs(path)
+    except OSError:
+        return False
+    return st.f_bavail * st.f_frsize >= margin * world * (HDR + 2 * slot_bytes)
+
+
 def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None) -> HostGather:
     """Collective once (torch.distributed): agree on a tag, create the
     segments, let dst attach them. No collective afterwards."""

@@ -175,3 +175,21 @@ def test_gloo_world3_host_gather():
             assert hdr.shape == (ne, 16) and rec.shape == (2 * ne, 12)
             assert np.all(hdr == 1000 * r + seq)
             np.testing.assert_array_equal(rec.reshape(-1), np.arange(2 * ne * 12) + 100 * seq)
+
+
+def test_host_gather_checks_shm_capacity(tmp_path):
+    """bench.py's host gather first checks that every rank's segment (a header
+    + two slots, page-locked in full) fits the node's shared-memory filesystem
+    and otherwise falls back to the RCCL gather: a tmpfs would accept the
+    segment and fail only when the copies touch its pages."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    from bgx import hostgather
+    slot = hostgather.slot_bytes_for(8192, 300)
+    assert slot >= 8192 * 600 * 48   # a record per lane-step since the last harvest + the open episodes
+    st = os.statvfs(str(tmp_path))
+    free = st.f_bavail * st.f_frsize
+    assert hostgather.shm_fits(1, 4096, path=str(tmp_path))
+    assert not hostgather.shm_fits(8, free, path=str(tmp_path))
+    assert not hostgather.shm_fits(2, slot, path=str(tmp_path / "missing"))
