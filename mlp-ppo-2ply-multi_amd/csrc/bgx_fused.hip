@@ -614,11 +614,14 @@ extern "C" int bgx_diag_stamps(unsigned long long* out32) {
 #endif
 
 extern "C" hipError_t bgx_launch_fused(const bgx::FusedArgs* args, hipStream_t stream) {
-    static int n_cu = 0;
+    // per device (one process may drive several GPUs: multi/worker.py gives
+    // worker 0 GPUs 0 and 7): the CU count and the kernels' dynamic-LDS opt-in
+    static int n_cu_dev[64] = {0};
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || cur < 0 || cur >= 64) cur = 0;
+    int& n_cu = n_cu_dev[cur];
     if (!n_cu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cur) != hipSuccess || n_cu <= 0)
             n_cu = 256;
         const void* k16[] = {(const void*)bgx::fused_step_kernel<false, 16>, (const void*)bgx::fused_step_kernel<true, 16>};
         const void* k32[] = {(const void*)bgx::fused_step_kernel<false, 32>, (const void*)bgx::fused_step_kernel<true, 32>};

@@ -360,13 +360,16 @@ __global__ __launch_bounds__(128) void value_f32_kernel(const float* __restrict_
 }  // namespace bgx
 
 extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t stream) {
-    static int n_cu = 0;
+    // per device (one process may drive several GPUs: multi/worker.py gives
+    // worker 0 GPUs 0 and 7): the CU count and the kernels' dynamic-LDS opt-in
+    static int n_cu_dev[64] = {0};
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || cur < 0 || cur >= 64) cur = 0;
+    int& n_cu = n_cu_dev[cur];
     const int lds = bgx::NFRAG * 16 + 256 * 16 + 128 * 4;
     const int lds_il = lds + bgx::IL_NW * 2 * bgx::IL_RB * 16;
     if (!n_cu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cur) != hipSuccess || n_cu <= 0)
             n_cu = 256;
         if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds) != hipSuccess ||
