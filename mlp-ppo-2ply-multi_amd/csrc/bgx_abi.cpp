@@ -1298,6 +1298,7 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
         f.hv_hdr = e->out_headers[b];
         f.hv_rec = e->out_records[b];
         f.hv_ep_cap = e->d.ep_cap;
+        f.hv_rec_cap = (long long)e->cfg.lanes * e->cfg.ring;
         f.hv_ctr = e->fh_ctr + b;
         f.hv_next = e->fh_ctr + (b + 1) % bgx_engine::NHB;
         f.hv_info = e->d_info[b];

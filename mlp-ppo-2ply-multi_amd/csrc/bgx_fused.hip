@@ -489,6 +489,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     ne = (int)(s.epi - s.hepi);
                     nr = (int)(s.ep_first - s.harv);
                 }
+                // a lane past its header ring or record ring (flagged when it
+                // happened) has lost episodes: nothing of this group is copied
+                const bool lost = ballot(ne > e.HR || nr > e.R) != 0ull;
+                if (lost) ne = nr = 0;
                 const int ie = wave_incl_scan(ne), ir = wave_incl_scan(nr);
                 const uint32_t te = (uint32_t)__shfl(ie, 63), tr = (uint32_t)__shfl(ir, 63);
                 if (l < FL) {
@@ -514,7 +518,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     if (pre[v + sstep] <= k) v += sstep;
                 return v;
             };
-            if (be + te <= (uint32_t)f.hv_ep_cap) {
+            // several launches between two tickets append to the same output:
+            // past its capacity (the caller did not harvest) nothing is copied
+            if ((unsigned long long)be + te <= (unsigned long long)f.hv_ep_cap &&
+                (unsigned long long)br + tr <= (unsigned long long)f.hv_rec_cap) {
                 for (uint32_t q = (uint32_t)t; q < 4u * te; q += NT) {   // 4 x uint4 per header
                     const uint32_t k = q >> 2;
                     const int v = owner(hs, k);

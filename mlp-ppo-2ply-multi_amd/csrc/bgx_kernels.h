@@ -179,7 +179,8 @@ struct FusedArgs {
     // output's counter. hv_hdr null: no harvest in this launch.
     uint32_t* hv_hdr;            // [ep cap][EP_WORDS]
     uint32_t* hv_rec;            // [L * R][REC_WORDS]
-    int hv_ep_cap;
+    int hv_ep_cap;               // headers the output holds
+    long long hv_rec_cap;        // records the output holds (L x R)
     unsigned long long* hv_ctr;  // this output's running totals
     unsigned long long* hv_next; // the next output's (zeroed by the last workgroup)
     uint32_t* hv_info;           // [4] device
