@@ -466,6 +466,24 @@ def test_fused_in_kernel_harvest_slots(weights_seed0):
             np.testing.assert_array_equal(got[key][1][f], want[key][1][f], err_msg=f"{key} {f}")
 
 
+def test_fused_harvest_past_capacity_is_an_error(weights_seed0):
+    """Several fused launches without a harvest append more finished episodes
+    than a small output holds (ep_cap = 64 headers): the in-kernel harvest
+    copies nothing past the output and the fetch reports BGX_E_STATE; the
+    engine keeps running and harvests normally afterwards."""
+    from bgx import BgxError
+    e = _engine(weights_seed0, lanes=64, seed=5, ply=1, fused=True, ep_cap=64, ring=512)
+    for _ in range(5):
+        e.step(200)
+    with pytest.raises(BgxError):
+        e.harvest()
+    e.step(40)
+    h = e.harvest()
+    assert 0 < h.n_episodes <= 64
+    e.sync()
+    e.close()
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_pipelined_harvest_equals_synchronous(weights_seed0, fused):
     """harvest_enqueue / harvest_fetch (the next step queued before the host
