@@ -878,6 +878,20 @@ int bgx_engine_destroy(bgx_engine* e) {
                     b_max = q[24] > b_max ? q[24] : b_max;
                     e_max = q[25] > e_max ? q[25] : e_max;
                 }
+                if (const char* path = getenv("BGX_FUSED_PROF_DUMP")) {
+                    // the last launch per workgroup: begin / end clocks (100 MHz),
+                    // loop start / end, rows, tier-2 jobs, lane-steps
+                    if (FILE* fp = fopen(path, "w")) {
+                        fprintf(fp, "wg,begin,end,loop0,loop1,rows,tier2,lane_steps\n");
+                        for (int b = 0; b < 1024; ++b) {
+                            const unsigned long long* q = &p[(size_t)b * 32];
+                            if (q[25] <= q[24]) continue;
+                            fprintf(fp, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", b, q[24], q[25], q[19], q[20], q[26],
+                                    q[27], q[28]);
+                        }
+                        fclose(fp);
+                    }
+                }
                 if (!dur.empty()) {
                     std::sort(dur.begin(), dur.end());
                     double mean = 0;
