@@ -487,7 +487,7 @@ def test_fused_harvest_past_capacity_is_an_error(weights_seed0):
 @pytest.mark.parametrize("fused", [True, False])
 def test_pipelined_harvest_equals_synchronous(weights_seed0, fused):
     """harvest_enqueue / harvest_fetch (the next step queued before the host
-    reads a harvest; two alternating buffers) deliver exactly the episodes of
+    reads a harvest; three rotating buffers) deliver exactly the episodes of
     the synchronous harvest(); a stale ticket is refused."""
     from bgx import BgxError
     a = _engine(weights_seed0, lanes=96, seed=29, ply=1, fused=fused)
