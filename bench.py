@@ -54,7 +54,6 @@ def load_weights():
 
 
 BACKEND = os.environ.get("BGX_DIST_BACKEND", "nccl")   # "gloo": rehearsal with ranks sharing GPUs
-GATHER_USED = [None]   # set when --gather host falls back to RCCL (run_engine)
 
 
 def _coll_device():
@@ -129,16 +128,10 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     hg = None
     if world > 1 and args.gather == "host":
         from bgx import hostgather
-        slot = hostgather.slot_bytes_for(lanes, args.harvest_every)
-        # rank 0 checks that every rank's segment fits the node's /dev/shm (a
-        # container's tmpfs can be small); all ranks follow its decision
-        import torch.distributed as dist
-        fits = [hostgather.shm_fits(world, slot) if rank == 0 else None]
-        dist.broadcast_object_list(fits, src=0)
-        if fits[0]:
-            hg = hostgather.setup(rank, world, slot, dst=0, device=torch.cuda.current_device())
-        else:
-            GATHER_USED[0] = "rccl (fallback: /dev/shm too small for the host gather's segments)"
+        # anonymous memory segments (memfd), not /dev/shm files: the path does
+        # not depend on the container's /dev/shm size (bgx/hostgather.py)
+        hg = hostgather.setup(rank, world, hostgather.slot_bytes_for(lanes, args.harvest_every), dst=0,
+                              device=torch.cuda.current_device())
     seq = [0]
 
     def run(n):
@@ -202,7 +195,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     s0 = eng.stats()
     barrier(world)
     t0 = time.perf_counter()
-    run(steps)          # graph-launched step sequence, no events in the stream
+    run(steps)          # direct launches, no events in the stream
     barrier(world)
     el = time.perf_counter() - t0
     s1 = eng.stats()
@@ -529,9 +522,8 @@ def main():
                        "engine": ("fused step kernel" + ("" if args.no_balance else ", balanced launches")
                                   if args.ply == 1 and not args.no_fused else "phased launches"),
                        "parallelism": ((f"lanes sharded x{world}, episode gather to rank 0 over the DMA engines "
-                                        f"into host shared memory" if args.gather == "host" and not GATHER_USED[0]
-                                        else f"lanes sharded x{world}, RCCL episode gather to rank 0 ({BACKEND}"
-                                        + (f"; {GATHER_USED[0]})" if GATHER_USED[0] else ")"))
+                                        f"into page-locked host memory (memfd segments)" if args.gather == "host"
+                                        else f"lanes sharded x{world}, RCCL episode gather to rank 0 ({BACKEND})")
                                        if world > 1 else "single GPU")},
             "desync_steps": head["desync_steps"],
             "world_size": world, "env_steps_per_rank": head["env_steps_per_rank"],

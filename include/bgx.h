@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 7
+#define BGX_ABI_VERSION 8
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -80,6 +80,15 @@ int bgx_movegen(const uint8_t* d_boards, const uint8_t* d_player, const uint8_t*
  * d_out is float32 [n][198]. */
 int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d_out, int layout,
                void* stream);
+
+/* bgx_encode on the engine's own packed boards (bgx_harvest records and
+ * headers, u32[8] each; the indicator player in word 6): for the callers that
+ * re-encode harvested observations (Episode.observation / next_observation,
+ * the trainer's inputs). Such boards come from the engine, so there is no
+ * input-domain check and no synchronization: asynchronous on `stream`, and
+ * capturable in a stream graph. Same values as bgx_encode of the unpacked
+ * board. */
+int bgx_encode_packed(const uint32_t* d_packed, int n, float* d_out, int layout, void* stream);
 
 /* ---------------- value network ---------------- */
 typedef struct bgx_net bgx_net;

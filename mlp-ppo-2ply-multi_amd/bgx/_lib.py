@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("BGX_LIB", os.path.join(_HERE, "libbgx.so"))
 c_int, c_float, c_double, c_u64, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                              ctypes.c_uint64, ctypes.c_void_p)
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class BgxError(RuntimeError):
@@ -58,6 +58,7 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_int32)]),
     "bgx_movegen": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "bgx_encode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "bgx_encode_packed": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "bgx_net_create": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_void_p)]),
     "bgx_net_destroy": (c_int, [c_void_p]),
     "bgx_value": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

@@ -7,7 +7,7 @@ winner at a terminal step), state_value / next_state_value Python floats,
 reward np.float32 0-d array, done bool. Episode carries win_type and
 close_out_counts / prime_reward_counts keyed by the players who made a
 decision (episode.py:56-76). Observations are re-encoded on the GPU from the
-packed boards (bgx_encode), not stored as 198 floats per step.
+packed boards (bgx_encode_packed), not stored as 198 floats per step.
 """
 from __future__ import annotations
 
@@ -23,7 +23,7 @@ from .records import REC_WORDS, WIN_TYPES
 def decode_records(headers, records: torch.Tensor):
     """Harvested episodes -> dict of host numpy arrays: the record fields
     (bgx/records.py) plus the boards before / after every move (u8 [m, 52])
-    and the 198-d observations, encoded on the device (bgx_encode).
+    and the 198-d observations, encoded on the device (bgx_encode_packed).
     headers: uint32/int32 [n, 16] (host or device); records int32 [m, 12]
     (device), each episode's records contiguous in header order."""
     hdr = headers.cpu().numpy() if isinstance(headers, torch.Tensor) else np.asarray(headers)
@@ -38,11 +38,10 @@ def decode_records(headers, records: torch.Tensor):
     dev = records.device
     b_t = torch.from_numpy(before.view(np.int32)).to(dev)
     a_t = torch.from_numpy(after.view(np.int32)).to(dev)
-    b8, a8 = ops.unpack(b_t), ops.unpack(a_t)
     out = records_np.fields(rec)
-    out.update(obs=ops.encode(b8, ops.packed_player(b_t)).cpu().numpy(),
-               next_obs=ops.encode(a8, ops.packed_player(a_t)).cpu().numpy(),
-               before=b8.cpu().numpy(), after=a8.cpu().numpy())
+    # engine-produced boards: the unchecked, asynchronous packed encoder
+    out.update(obs=ops.encode_packed(b_t).cpu().numpy(), next_obs=ops.encode_packed(a_t).cpu().numpy(),
+               before=ops.unpack(b_t).cpu().numpy(), after=ops.unpack(a_t).cpu().numpy())
     return out
 
 

@@ -5,15 +5,24 @@ The reference hands finished episodes from its 7 workers to main.py through a
 pickled multiprocessing.Queue (src/main.py:115-133,
 src/multi/experience_queue.py:5-13): a host-side hand-off. Here every rank
 runs its own Engine on its GPU; after a harvest it copies the compact
-headers (64 B) and records (48 B) device -> host straight into a
-shared-memory segment that is page-locked for DMA (bgx_host_register), on a
-DMA engine (bgx_dma_copy_d2h: SDMA through the HSA runtime, so the transfer
-runs while the persistent fused kernel holds every compute unit; the HIP
-runtime here would serve hipMemcpyAsync with a blit kernel, which waits for
-free compute units — BGX_HG_COPY=hip selects that path).
-The counts travel in the same segment: there is no per-harvest collective.
-The trainer rank reads every peer's batch from host memory (where main.py's
-consumer wants them) and acknowledges it.
+headers (64 B) and records (48 B) device -> host straight into a host
+segment that is page-locked for DMA (bgx_host_register), on a DMA engine
+(bgx_dma_copy_d2h: SDMA through the HSA runtime, so the transfer runs while
+the persistent fused kernel holds every compute unit; the HIP runtime here
+would serve hipMemcpyAsync with a blit kernel, which waits for free compute
+units — BGX_HG_COPY=hip selects that path). The counts travel in the same
+segment: there is no per-harvest collective. The trainer rank reads every
+peer's batch from host memory (where main.py's consumer wants them) and
+acknowledges it.
+
+Segments are anonymous memory files (memfd_create), not /dev/shm files: a
+container's /dev/shm is often a 64 MB tmpfs, while a rank's segment is
+~0.5 GB at 8,192 lanes, and a tmpfs accepts a larger file and fails only when
+its pages are touched. A memfd is limited by the host's memory alone. Each
+rank creates its own; the trainer rank receives the peers' descriptors once,
+at setup, over a Unix socket (SCM_RIGHTS) and maps them. So the host path
+has no capacity-dependent fallback: bench.py --gpus N takes it whatever
+/dev/shm holds (tests/test_gpu_dist.py runs it with two ranks on one GPU).
 
 Protocol (per rank r != dst, batch numbers 1, 2, ... ; two slots):
   publish(h): wait until dst acknowledged batch seq - 2 (the slot's previous
@@ -30,10 +39,11 @@ other slot's.
 """
 from __future__ import annotations
 
+import mmap
 import os
 import secrets
+import socket
 import time
-from multiprocessing import shared_memory
 
 import numpy as np
 import torch
@@ -55,9 +65,15 @@ def slot_bytes_for(lanes: int, steps_per_harvest: int, max_steps: int = 300) -> 
 
 
 class Pending:
-    def __init__(self, gather, seq, n_eps, n_recs, slot, event, dma=()):
+    """A batch in flight. It holds the source arrays (`keep`) until wait()
+    has seen the copies finish: the caller may drop its Harvest at once, and
+    the caching allocator cannot hand the blocks to anything else while a DMA
+    engine still reads them."""
+
+    def __init__(self, gather, seq, n_eps, n_recs, slot, event, dma=(), keep=None):
         self.g, self.seq, self.n_eps, self.n_recs, self.slot, self.event = gather, seq, n_eps, n_recs, slot, event
         self.dma = dma
+        self.keep = keep
 
     def wait(self):
         if self.event is not None:
@@ -67,10 +83,37 @@ class Pending:
             for t in self.dma:
                 check(lib().bgx_dma_wait(t, int(self.g.timeout * 1000)), "bgx_dma_wait")
             self.dma = ()
+        self.keep = None
         c = self.g.ctrl[self.g.rank]
         c[1 + 2 * self.slot], c[2 + 2 * self.slot] = self.n_eps, self.n_recs
         c[0] = self.seq            # publishes (aligned 8-byte store after the counts)
         return self.seq
+
+
+class _Segment:
+    """An anonymous shared memory file (memfd) mapped into this process."""
+
+    def __init__(self, name, size=None, fd=None):
+        if fd is None:
+            fd = os.memfd_create(name, os.MFD_CLOEXEC)
+            os.ftruncate(fd, size)
+        else:
+            size = os.fstat(fd).st_size
+        self.fd, self.size = fd, size
+        self.mm = mmap.mmap(fd, size, flags=mmap.MAP_SHARED, prot=mmap.PROT_READ | mmap.PROT_WRITE)
+        self.buf = memoryview(self.mm)
+
+    def close(self):
+        # (views a caller still holds keep the mapping; it goes with the process)
+        for f in (self.buf.release, self.mm.close):
+            try:
+                f()
+            except (BufferError, ValueError):
+                pass
+        try:
+            os.close(self.fd)
+        except OSError:
+            pass
 
 
 class HostGather:
@@ -84,8 +127,7 @@ class HostGather:
         self.timeout = timeout
         self.device = device
         self.seq = 0
-        self._mine = shared_memory.SharedMemory(name=self._name(rank), create=True,
-                                                size=HDR + 2 * self.slot_bytes)
+        self._mine = _Segment(self._name(rank), size=HDR + 2 * self.slot_bytes)
         self.shm = {rank: self._mine}
         np.ndarray((8,), np.int64, buffer=self._mine.buf[:HDR])[:] = 0
         self.ctrl = {rank: np.ndarray((8,), np.int64, buffer=self._mine.buf[:HDR])}
@@ -104,15 +146,42 @@ class HostGather:
     def _name(self, r):
         return f"bgx_hg_{self.tag}_{r}"
 
-    def attach(self):
-        """dst: open every peer's segment (after all ranks constructed theirs)."""
+    def _sock_name(self):
+        return f"\0{self._name('dst')}".encode()
+
+    def listen(self):
+        """dst, before the peers connect: the socket that receives their segments."""
         if self.rank != self.dst:
             return
-        for r in range(self.world):
-            if r not in self.shm:
-                s = shared_memory.SharedMemory(name=self._name(r))
+        self._listener = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self._listener.bind(self._sock_name())   # abstract namespace: no file, no /dev/shm
+        self._listener.listen(self.world)
+
+    def send_segment(self):
+        """Rank != dst: hand this rank's segment descriptor to dst (SCM_RIGHTS)."""
+        if self.rank == self.dst:
+            return
+        with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as so:
+            so.settimeout(self.timeout)
+            so.connect(self._sock_name())
+            socket.send_fds(so, [int(self.rank).to_bytes(4, "little")], [self._mine.fd])
+            so.recv(1)   # dst has mapped it
+
+    def attach(self):
+        """dst: receive and map every peer's segment (after listen())."""
+        if self.rank != self.dst:
+            return
+        self._listener.settimeout(self.timeout)
+        for _ in range(self.world - 1):
+            conn, _addr = self._listener.accept()
+            with conn:
+                msg, fds, _flags, _addr = socket.recv_fds(conn, 4, 1)
+                r = int.from_bytes(msg, "little")
+                s = _Segment(None, fd=fds[0])
                 self.shm[r] = s
                 self.ctrl[r] = np.ndarray((8,), np.int64, buffer=s.buf[:HDR])
+                conn.sendall(b"k")
+        self._listener.close()
 
     def _slot(self, r, slot):
         base = HDR + slot * self.slot_bytes
@@ -134,14 +203,14 @@ class HostGather:
         """Rank != dst: start the copy of a Harvest into this rank's segment.
         ready=True: the harvest's device arrays are complete (bgx_harvest_fetch
         waited for them); otherwise the current stream is synchronized first."""
+        n_eps, n_recs = h.n_episodes, h.n_records
+        need = n_eps * EP_BYTES + n_recs * REC_BYTES
+        if need > self.slot_bytes:   # before the batch number moves: dst still waits for the same batch
+            raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")
         self.seq += 1
         seq, slot = self.seq, self.seq % 2
         c = self.ctrl[self.rank]
         self._spin(lambda: int(c[5]) >= seq - 2, f"dst did not read batch {seq - 2}")
-        n_eps, n_recs = h.n_episodes, h.n_records
-        need = n_eps * EP_BYTES + n_recs * REC_BYTES
-        if need > self.slot_bytes:
-            raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")
         dst = np.frombuffer(self._slot(self.rank, slot), np.uint8)
         if n_eps == 0:
             return Pending(self, seq, 0, 0, slot, None)
@@ -158,12 +227,16 @@ class HostGather:
                   "bgx_dma_copy_d2h")
             check(lib().bgx_dma_copy_d2h(base + n_eps * EP_BYTES, h.records.data_ptr(), n_recs * REC_BYTES, dev,
                                          ctypes.byref(t2)), "bgx_dma_copy_d2h")
-            return Pending(self, seq, n_eps, n_recs, slot, None, dma=(t1.value, t2.value))
+            return Pending(self, seq, n_eps, n_recs, slot, None, dma=(t1.value, t2.value),
+                           keep=(h.headers, h.records))
         if h.headers.is_cuda and self._stream is not None:
             from ._lib import check, lib
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(h.headers.device))
             self._stream.wait_event(ev)
+            # the side stream reads the arrays: the allocator must not reuse them before it is done
+            h.headers.record_stream(self._stream)
+            h.records.record_stream(self._stream)
             base = dst.ctypes.data
             s = self._stream.cuda_stream
             check(lib().bgx_copy_async(base, h.headers.data_ptr(), n_eps * EP_BYTES, COPY_KIND, s),
@@ -174,7 +247,7 @@ class HostGather:
             done.record(self._stream)
             # the engine's buffers must outlive the copy: the caller waits this
             # Pending before its next harvest (bgx_harvest reuses them)
-            return Pending(self, seq, n_eps, n_recs, slot, done)
+            return Pending(self, seq, n_eps, n_recs, slot, done, keep=(h.headers, h.records))
         hb = h.headers.cpu().numpy().view(np.uint8).reshape(-1)
         rb = h.records.cpu().numpy().view(np.uint8).reshape(-1)
         dst[:hb.size] = hb
@@ -216,19 +289,13 @@ class HostGather:
             from ._lib import lib
             lib().bgx_host_unregister(self._registered)
             self._registered = None
-        for r, s in list(self.shm.items()):
-            try:
-                if r != self.rank:
-                    s.close()
-            except (BufferError, OSError):
-                pass
         self.ctrl = {}
-        try:
-            self._mine.close()
-            self._mine.unlink()
-        except (BufferError, FileNotFoundError, OSError):
-            pass
+        for s in list(self.shm.values()):
+            s.close()
         self.shm = {}
+        lst = getattr(self, "_listener", None)
+        if lst is not None:
+            lst.close()
 
 
 def make_tag() -> str:
@@ -236,26 +303,16 @@ def make_tag() -> str:
     return f"{os.getpid()}_{secrets.token_hex(4)}"
 
 
-def shm_fits(world: int, slot_bytes: int, path: str = "/dev/shm", margin: float = 1.25) -> bool:
-    """Whether the node's shared-memory filesystem has room for every rank's
-    segment (a header + two slots each, page-locked in full). A tmpfs accepts
-    a larger segment at creation and fails only when its pages are touched,
-    so the launcher checks first and otherwise uses the RCCL gather."""
-    try:
-        st = os.statvfs(path)
-    except OSError:
-        return False
-    return st.f_bavail * st.f_frsize >= margin * world * (HDR + 2 * slot_bytes)
-
-
 def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None) -> HostGather:
     """Collective once (torch.distributed): agree on a tag, create the
-    segments, let dst attach them. No collective afterwards."""
+    segments, hand their descriptors to dst. No collective afterwards."""
     import torch.distributed as dist
     obj = [make_tag() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     g = HostGather(rank, world, obj[0], slot_bytes, dst=dst, device=device)
+    g.listen()
     dist.barrier()
+    g.send_segment()
     g.attach()
     dist.barrier()
     return g

@@ -69,6 +69,22 @@ def encode(boards, player, layout: int = 0, stream=None):
     return out
 
 
+def encode_packed(packed, layout: int = 0, stream=None):
+    """encode() of the engine's own packed boards (int32 [n, 8]: harvest
+    records / headers, the indicator in word 6): no input-domain check and no
+    synchronization (bgx_encode_packed; such boards come from the engine)."""
+    packed = torch.as_tensor(packed)
+    if not packed.is_cuda:
+        packed = packed.cuda()
+    packed = packed.contiguous().view(-1, 8)
+    require_cuda(packed)
+    n = packed.shape[0]
+    out = torch.empty((n, 198), dtype=torch.float32, device=packed.device)
+    check(lib().bgx_encode_packed(ptr(packed), n, ptr(out), int(layout), stream_handle(stream)),
+          "bgx_encode_packed")
+    return out
+
+
 def pack(boards, player, stream=None):
     boards, player = _u8(boards).view(-1, 52), _u8(player).view(-1)
     require_cuda(boards, player)

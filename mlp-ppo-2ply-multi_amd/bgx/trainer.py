@@ -63,7 +63,7 @@ class DeviceTrainer:
             rec = rec.view(torch.int32) if rec.dtype == torch.uint32 else rec.to(torch.int32)
         before = torch.zeros((rec.shape[0], 8), dtype=torch.int32, device=self.device)
         before[:, :7] = rec[:, :7]   # the board before the move, the mover's indicator (bgx/records.py)
-        obs = ops.encode(ops.unpack(before), ops.packed_player(before))
+        obs = ops.encode_packed(before)
         rewards = rec[:, 9].contiguous().view(torch.float32)
         hdr = np.asarray(torch.as_tensor(headers).cpu().numpy()).astype(np.uint32)
         lens = hdr[:, 3].astype(np.int64).tolist()

@@ -175,7 +175,9 @@ struct bgx_engine {
     uint32_t* h_info = nullptr;    // [NHB][4] host-mapped copies, written by the harvesting kernel itself
     uint32_t* h_info_dev = nullptr;   // its device address
     // fused engine (in-kernel harvest): per slot the running {episodes << 32 |
-    // records} appended since the previous ticket, [NHB] = finished workgroups
+    // records} appended since the previous ticket, [NHB] = finished workgroups,
+    // [NHB + 1 + b] = slot b's accumulated error flags (moved there from the
+    // engine's word by each launch's last workgroup)
     unsigned long long* fh_ctr = nullptr;
     bool fh_launched = false;      // a fused launch filled the current slot since the last ticket
     hipEvent_t hev = nullptr;         // the engine's last step, for a harvest on another stream
@@ -212,14 +214,22 @@ static int flag_error(unsigned f) {
                 "16 episode list, 32 scripted dice: capacity; 64 an intra-workgroup wait hit its bound: state)", f);
 }
 
+// after the engine's stream is synchronized: the flags raised since the last
+// harvest ticket (they move into a ticket's totals when it is harvested, and
+// bgx_harvest_fetch reports them there). The engine word is reset here; a
+// fused engine's launches have already moved theirs into the open ticket's
+// accumulator, which is reported but left for the ticket.
 static int check_flags(bgx_engine* e) {
     unsigned f = 0;
     HIP_TRY(hipMemcpy(&f, e->ctr + C_ERR, 4, hipMemcpyDeviceToHost));
-    if (f) {
-        HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
-        return flag_error(f);
+    if (f) HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
+    if (e->fh_ctr) {
+        unsigned long long acc = 0;
+        HIP_TRY(hipMemcpy(&acc, e->fh_ctr + bgx_engine::NHB + 1 + e->h_tickets % bgx_engine::NHB, 8,
+                          hipMemcpyDeviceToHost));
+        f |= (unsigned)acc;
     }
-    return BGX_OK;
+    return f ? flag_error(f) : BGX_OK;
 }
 
 
@@ -422,6 +432,12 @@ int dma_setup(int dev, DmaDev** out) {
         q.domain = (uint32_t)dom;
         hsa_iterate_agents(find_agents, &q);
         if (!q.have_gpu || !q.have_cpu) return fail(BGX_E_STATE, "bgx_dma: no HSA agent for device %d", dev);
+        // the CPU agent of the GPU's own NUMA node (a multi-socket host lists one
+        // CPU agent per node; the first one found may be the far socket)
+        hsa_agent_t near{};
+        if (hsa_agent_get_info(q.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NEAREST_CPU, &near) == HSA_STATUS_SUCCESS &&
+            near.handle != 0)
+            q.cpu = near;
         uint32_t mask = 0;
         if (hsa_amd_memory_copy_engine_status(q.cpu, q.gpu, &mask) != HSA_STATUS_SUCCESS || mask == 0)
             return fail(BGX_E_STATE, "bgx_dma: no DMA engine available for device %d -> host", dev);
@@ -525,6 +541,19 @@ int bgx_encode(const uint8_t* d_boards, const uint8_t* d_player, int n, float* d
         if (int rc = lease_scratch((hipStream_t)stream, L)) return rc;
         if (int rc = require_domain("bgx_encode", L.sc, d_boards, d_player, nullptr, n, (hipStream_t)stream)) return rc;
         HIP_TRY(bgx_launch_encode(d_boards, d_player, n, d_out, layout, (hipStream_t)stream));
+        return BGX_OK;
+    });
+}
+
+int bgx_encode_packed(const uint32_t* d_packed, int n, float* d_out, int layout, void* stream) {
+    return guarded("bgx_encode_packed", [&]() -> int {
+        if (n < 0 || (layout != 0 && layout != 1))
+            return fail(BGX_E_ARG, "bgx_encode_packed: n=%d layout=%d", n, layout);
+        if (n == 0) return BGX_OK;
+        if (!d_packed || !d_out) return fail(BGX_E_ARG, "bgx_encode_packed: null pointer");
+        DeviceScope ds(d_packed);
+        HIP_TRY(ds.err);
+        HIP_TRY(bgx_launch_encode_packed(d_packed, n, d_out, layout, (hipStream_t)stream));
         return BGX_OK;
     });
 }
@@ -862,6 +891,16 @@ int bgx_engine_destroy(bgx_engine* e) {
                     fprintf(stderr, "[bgx fused prof] choice per wave-step: state + Philox refill %.2f, pick %.2f, "
                             "env step %.2f us\n", c[0] / nws / 100, c[1] / nws / 100, c[2] / nws / 100);
                 }
+                {
+                    double c[3] = {0, 0, 0};
+                    for (int b = 0; b < 1024; ++b) {
+                        c[0] += (double)p[(size_t)b * 32 + 6];
+                        c[1] += (double)p[(size_t)b * 32 + 22];
+                        c[2] += (double)p[(size_t)b * 32 + 23];
+                    }
+                    fprintf(stderr, "[bgx fused prof] MLP tiles per workgroup step: rows + k mask %.2f, MFMA chain issue %.2f, "
+                            "drain + epilogue %.2f wave-us\n", c[0] / n / 100, c[1] / n / 100, c[2] / n / 100);
+                }
                 fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
                         s[11] / (s[12] > 0 ? s[12] : 1) / 100);
                 fprintf(stderr, "[bgx fused prof] tier-1 job: doubles %.2f us (%.0f jobs), non-doubles %.2f us (%.0f jobs)\n",
@@ -1042,7 +1081,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             d.HR = hr;
             ALLOC(d.hring, (size_t)L * hr * bgx::EP_WORDS);
             ALLOC(d.hepi, L);
-            ALLOC(e->fh_ctr, bgx_engine::NHB + 1);
+            ALLOC(e->fh_ctr, 2 * bgx_engine::NHB + 1);
         }
         if (cfg->ply == 2) {
             e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
@@ -1065,7 +1104,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             return rc;
         }
         if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess ||
-            (e->fh_ctr && hipMemset(e->fh_ctr, 0, (bgx_engine::NHB + 1) * sizeof(unsigned long long)) != hipSuccess)) {
+            (e->fh_ctr && hipMemset(e->fh_ctr, 0, (2 * bgx_engine::NHB + 1) * sizeof(unsigned long long)) != hipSuccess)) {
             bgx_engine_destroy(e);
             return fail(BGX_E_HIP, "hipMemset failed");
         }
@@ -1315,6 +1354,8 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
         f.hv_rec_cap = (long long)e->cfg.lanes * e->cfg.ring;
         f.hv_ctr = e->fh_ctr + b;
         f.hv_next = e->fh_ctr + (b + 1) % bgx_engine::NHB;
+        f.hv_flags = e->fh_ctr + bgx_engine::NHB + 1 + b;
+        f.hv_next_flags = e->fh_ctr + bgx_engine::NHB + 1 + (b + 1) % bgx_engine::NHB;
         f.hv_info = e->d_info[b];
         f.hv_hinfo = e->h_info_dev + 4 * b;
         f.done_ctr = e->fh_ctr + bgx_engine::NHB;
@@ -1408,8 +1449,10 @@ int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream) {
             // the fused launches since the last ticket harvested into slot b and
             // published its totals; with none, publish the (empty) slot here
             if (!e->fh_launched)
-                HIP_TRY(bgx_launch_harvest_close(e->fh_ctr + b, e->fh_ctr + (b + 1) % bgx_engine::NHB, e->ctr + C_ERR,
-                                                 e->d_info[b], e->h_info_dev + 4 * b, s));
+                HIP_TRY(bgx_launch_harvest_close(e->fh_ctr + b, e->fh_ctr + (b + 1) % bgx_engine::NHB,
+                                                 e->fh_ctr + bgx_engine::NHB + 1 + b,
+                                                 e->fh_ctr + bgx_engine::NHB + 1 + (b + 1) % bgx_engine::NHB,
+                                                 e->ctr + C_ERR, e->d_info[b], e->h_info_dev + 4 * b, s));
             e->fh_launched = false;
         } else {
             HIP_TRY(bgx_launch_harvest_scan(&e->d, e->d_offs[b], e->d_info[b], e->h_info_dev + 4 * b, s));
@@ -1433,12 +1476,11 @@ int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out) {
         HIP_TRY(hipSetDevice(e->device));
         const int b = ticket % bgx_engine::NHB;
         HIP_TRY(hipEventSynchronize(e->hdone[b]));
+        // the ticket's own flags: its harvest (or the last launch before it)
+        // moved them out of the engine word on the device, in stream order
         const uint32_t* info = e->h_info + 4 * b;
         const uint32_t flags = info[2];
-        if (flags) {
-            HIP_TRY(hipMemset(e->ctr + C_ERR, 0, 4));
-            return flag_error(flags);
-        }
+        if (flags) return flag_error(flags);
         out->n_episodes = (int)info[0];
         out->n_records = (int)info[1];
         out->d_headers = e->out_headers[b];

@@ -74,6 +74,67 @@ __global__ __launch_bounds__(256) void encode_kernel(const uint8_t* __restrict__
     }
 }
 
+// The engine's own packed boards (records, candidate rows) straight to
+// features: one thread per (row, 4-feature quad), the row's two dwordx4 loads
+// shared through L1 by the 50 quads of a row; the point count is the nibble of
+// point i of player pl (word 3 pl + i / 8), bars / borne-off / the indicator
+// come from word 6. Same values as encode_kernel on the unpacked board.
+BGX_DEV float feature_packed(const uint32_t* w, int layout, int f) {
+    const uint32_t s6 = w[6];
+    const int player = (int)((s6 >> 16) & 1u);
+    int pl, rest;
+    if (f >= 196) return (f - 196) == player ? 1.0f : 0.0f;
+    if (layout == 0) {
+        if (f < 192) { pl = f / 96; rest = f - 96 * pl; }
+        else {
+            const int k = f - 192;   // bar1, off1, bar2, off2
+            const int who = k >> 1;
+            return (k & 1) ? kOff15[(s6 >> (8 + 4 * who)) & 15u] : (float)((s6 >> (4 * who)) & 15u) * 0.5f;
+        }
+    } else {
+        pl = f / 98;
+        rest = f - 98 * pl;
+        if (rest == 96) return (float)((s6 >> (4 * pl)) & 15u) * 0.5f;
+        if (rest == 97) return kOff15[(s6 >> (8 + 4 * pl)) & 15u];
+    }
+    const int i = rest >> 2;
+    const int n = (int)((w[3 * pl + (i >> 3)] >> (4 * (i & 7))) & 15u);
+    switch (rest & 3) {
+        case 0: return n >= 1 ? 1.0f : 0.0f;
+        case 1: return n >= 2 ? 1.0f : 0.0f;
+        case 2: return n >= 3 ? 1.0f : 0.0f;
+        default: return n > 3 ? (float)(n - 3) * 0.5f : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void encode_packed_kernel(const uint32_t* __restrict__ packed, int n,
+                                                            float* __restrict__ out, int layout) {
+    const size_t total = (size_t)n * 198;
+    const size_t stride = (size_t)gridDim.x * blockDim.x * 4;
+    for (size_t g = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; g < total; g += stride) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const size_t e = g + q;
+            if (e < total) {
+                const int row = (int)(e / 198);
+                const int f = (int)(e - (size_t)row * 198);
+                const uint4* p = (const uint4*)(packed + (size_t)row * 8);
+                const uint4 x = p[0], y = p[1];
+                const uint32_t w[7] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z};
+                v[q] = feature_packed(w, layout, f);
+            } else {
+                v[q] = 0.0f;
+            }
+        }
+        if (g + 4 <= total) {
+            *(float4*)(out + g) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (int q = 0; q < 4 && g + q < total; ++q) out[g + q] = v[q];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ boards,
                                                    const uint8_t* __restrict__ player, int n,
                                                    uint32_t* __restrict__ out) {
@@ -141,6 +202,17 @@ extern "C" hipError_t bgx_launch_encode(const uint8_t* boards, const uint8_t* pl
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(bgx::encode_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, boards, player,
                        n, out, layout);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t bgx_launch_encode_packed(const uint32_t* packed, int n, float* out, int layout,
+                                               hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const size_t quads = ((size_t)n * 198 + 3) / 4;
+    size_t blocks = (quads + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(bgx::encode_packed_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, packed, n, out,
+                       layout);
     return hipGetLastError();
 }
 

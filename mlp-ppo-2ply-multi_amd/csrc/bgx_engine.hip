@@ -341,7 +341,10 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
     }
     if (t == 0) {
         offs[n] = carry;
-        const uint32_t v[4] = {(uint32_t)n, (uint32_t)carry, *e.err_flags, n_raw};
+        // the flags of the steps since the previous harvest move into this one's
+        // totals (exchanged with 0 in stream order: no host reset of the word
+        // while the next step may already run)
+        const uint32_t v[4] = {(uint32_t)n, (uint32_t)carry, atomicExch(e.err_flags, 0u), n_raw};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             info[k] = v[k];
@@ -384,25 +387,32 @@ __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t
 }
 
 // in-kernel harvest (fused engine) with no fused launch since the last ticket:
-// the ticket's totals are whatever its counter holds (nothing was appended)
-__global__ void harvest_close_kernel(unsigned long long* ctr, unsigned long long* next, const unsigned* err_flags,
-                                     uint32_t* info, uint32_t* hinfo) {
+// the ticket's totals are whatever its counter holds (nothing was appended);
+// its flags are the accumulator plus any flag raised since (moved, not copied)
+__global__ void harvest_close_kernel(unsigned long long* ctr, unsigned long long* next, unsigned long long* flags,
+                                     unsigned long long* next_flags, unsigned* err_flags, uint32_t* info,
+                                     uint32_t* hinfo) {
     const unsigned long long c = *ctr;
-    const uint32_t v[4] = {(uint32_t)(c >> 32), (uint32_t)c, *err_flags, (uint32_t)(c >> 32)};
+    const uint32_t fl = atomicExch(err_flags, 0u) | (uint32_t)*flags;
+    *flags = fl;
+    const uint32_t v[4] = {(uint32_t)(c >> 32), (uint32_t)c, fl, (uint32_t)(c >> 32)};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         info[k] = v[k];
         if (hinfo) hinfo[k] = v[k];
     }
     *next = 0ull;
+    *next_flags = 0ull;
 }
 
 }  // namespace bgx
 
 extern "C" hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next,
-                                               const unsigned* err_flags, uint32_t* info, uint32_t* hinfo,
+                                               unsigned long long* flags, unsigned long long* next_flags,
+                                               unsigned* err_flags, uint32_t* info, uint32_t* hinfo,
                                                hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::harvest_close_kernel, dim3(1), dim3(1), 0, stream, ctr, next, err_flags, info, hinfo);
+    hipLaunchKernelGGL(bgx::harvest_close_kernel, dim3(1), dim3(1), 0, stream, ctr, next, flags, next_flags, err_flags,
+                       info, hinfo);
     return hipGetLastError();
 }
 

@@ -123,6 +123,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tc = 0, tw[4] = {0, 0, 0, 0}, t2c = 0, t3n = 0;
     unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
     unsigned long long tcs[3] = {0, 0, 0};      // choice: state + Philox refill, pick, env step (lane_advance)
+    unsigned long long tms[3] = {0, 0, 0};      // MLP tile: rows + k mask, MFMA chain issue, drain + epilogue
     constexpr bool prof = PROF;
     auto tick = [&](int k) {
         if (prof && t == 0) {
@@ -324,7 +325,21 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             bx = ((const uint4*)src)[0];
                             by = ((const uint4*)src)[1];
                         }
-                        const float v = mlp_tile4(wf, T.lut, T.w2s, f.feat_scale, bx, by, tile_kmask(bx, by));
+                        const uint32_t km = tile_kmask(bx, by);
+                        unsigned long long i1 = 0, i2 = 0;
+                        if (prof) {
+                            __builtin_amdgcn_s_waitcnt(0);
+                            i1 = wall_clock64();
+                            tms[0] += i1 - i0;   // rows loaded, lane_of, k mask
+                        }
+                        const float v = mlp_tile4<PROF>(wf, T.lut, T.w2s, f.feat_scale, bx, by, km, &i2);
+                        if (prof) {
+                            const float vv = __shfl(v, 0);   // the epilogue's value is ready
+                            asm volatile("" ::"v"(vv));
+                            const unsigned long long i3 = wall_clock64();
+                            tms[1] += i2 - i1;   // MFMA chain issued
+                            tms[2] += i3 - i2;   // drain + epilogue
+                        }
                         if (l < 32 && r < nr) {
                             const float val = v + f.b2;
                             if (k < XS) xs[vl * XS + k] = val;
@@ -481,17 +496,18 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             // the lanes' header rings, records from their record rings) appended to
             // the ticket's output at offsets from one 64-bit atomic, while other
             // workgroups still run their last steps (the scratch is free here)
-            uint32_t* hs = (uint32_t*)lds;   // [0, 64) episode prefix, [64, 128) record prefix, [128, 132) totals
+            uint32_t* hs = (uint32_t*)lds;   // [0, 64) episode prefix, [64, 128) record prefix, [128, 133) totals
             if (w == 0) {
                 int ne = 0, nr = 0;
+                bool lost = false;
                 if (l < nlive) {
                     const LaneState& s = T.st[l];
                     ne = (int)(s.epi - s.hepi);
                     nr = (int)(s.ep_first - s.harv);
+                    // past its header ring or record ring (flagged when it happened):
+                    // this lane's finished episodes are gone; only it is left out
+                    lost = ne > e.HR || nr > e.R;
                 }
-                // a lane past its header ring or record ring (flagged when it
-                // happened) has lost episodes: nothing of this group is copied
-                const bool lost = ballot(ne > e.HR || nr > e.R) != 0ull;
                 if (lost) ne = nr = 0;
                 const int ie = wave_incl_scan(ne), ir = wave_incl_scan(nr);
                 const uint32_t te = (uint32_t)__shfl(ie, 63), tr = (uint32_t)__shfl(ir, 63);
@@ -500,16 +516,38 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     hs[64 + l] = (uint32_t)(ir - nr);
                 }
                 if (l == 0) {
-                    const unsigned long long base =
-                        te | tr ? atomicAdd(f.hv_ctr, ((unsigned long long)te << 32) | tr) : 0ull;
+                    // the group's place in the ticket's output, reserved only if the
+                    // whole group fits (several launches between two tickets append
+                    // to one output); a group that does not fit keeps its episodes
+                    // in the rings for the next ticket
+                    unsigned long long base = 0ull;
+                    uint32_t fit = 1u;
+                    if (te | tr) {
+                        unsigned long long old = __hip_atomic_load(f.hv_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        for (;;) {
+                            if ((old >> 32) + te > (unsigned long long)f.hv_ep_cap ||
+                                (old & 0xFFFFFFFFull) + tr > (unsigned long long)f.hv_rec_cap) {
+                                fit = 0u;
+                                break;
+                            }
+                            const unsigned long long prev = atomicCAS(f.hv_ctr, old, old + (((unsigned long long)te << 32) | tr));
+                            if (prev == old) {
+                                base = old;
+                                break;
+                            }
+                            old = prev;
+                        }
+                    }
                     hs[128] = te;
                     hs[129] = tr;
                     hs[130] = (uint32_t)(base >> 32);
                     hs[131] = (uint32_t)base;
+                    hs[132] = fit;
                 }
+                if (l < FL) hs[136 + l] = lost ? 1u : 0u;
             }
             __syncthreads();
-            const uint32_t te = hs[128], tr = hs[129], be = hs[130], br = hs[131];
+            const uint32_t te = hs[128], tr = hs[129], be = hs[130], br = hs[131], fit = hs[132];
             // lane of the k-th episode / record: the last v with prefix[v] <= k
             auto owner = [&](const uint32_t* pre, uint32_t k) -> int {
                 int v = 0;
@@ -518,10 +556,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     if (pre[v + sstep] <= k) v += sstep;
                 return v;
             };
-            // several launches between two tickets append to the same output:
-            // past its capacity (the caller did not harvest) nothing is copied
-            if ((unsigned long long)be + te <= (unsigned long long)f.hv_ep_cap &&
-                (unsigned long long)br + tr <= (unsigned long long)f.hv_rec_cap) {
+            if (fit) {
                 for (uint32_t q = (uint32_t)t; q < 4u * te; q += NT) {   // 4 x uint4 per header
                     const uint32_t k = q >> 2;
                     const int v = owner(hs, k);
@@ -538,12 +573,12 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                         (const uint4*)(e.ring + ((size_t)(g * FL + v) * e.R + (rr & (uint32_t)(e.R - 1))) * REC_WORDS);
                     ((uint4*)(f.hv_rec + (size_t)(br + r) * REC_WORDS))[c] = src[c];
                 }
-            } else if (t == 0) {
-                atomicOr(e.err_flags, BGX_ERRF_EPISODE_LIST);
             }
             for (int v = t; v < nlive; v += NT) {
-                e.harv[g * FL + v] = T.st[v].ep_first;
-                e.hepi[g * FL + v] = T.st[v].epi;
+                if (fit || hs[136 + v]) {   // harvested (or lost): the marks move on
+                    e.harv[g * FL + v] = T.st[v].ep_first;
+                    e.hepi[g * FL + v] = T.st[v].epi;
+                }
             }
         }
         __syncthreads();
@@ -572,6 +607,9 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             for (int k = 0; k < 4; ++k) atomicAdd(P + 7 + k, tw[k]);
             for (int k = 0; k < 4; ++k) atomicAdd(P + 14 + k, tjd[k]);
             for (int k = 0; k < 3; ++k) atomicAdd(P + 29 + k, tcs[k]);
+            atomicAdd(P + 6, tms[0]);
+            atomicAdd(P + 22, tms[1]);
+            atomicAdd(P + 23, tms[2]);
         }
     }
     if (t == 0) {
@@ -589,7 +627,11 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 if (f.budget > 0) __hip_atomic_store(f.budget_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (f.hv_hdr) {
                     const unsigned long long c = __hip_atomic_load(f.hv_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t fl = __hip_atomic_load(e.err_flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // the launch's flags move into this ticket's accumulator (stream
+                    // order: the fetch never resets the engine word behind a launch)
+                    const uint32_t fl = atomicExch(e.err_flags, 0u) | (uint32_t)*f.hv_flags;
+                    *f.hv_flags = fl;
+                    *f.hv_next_flags = 0ull;
                     const uint32_t v[4] = {(uint32_t)(c >> 32), (uint32_t)c, fl, (uint32_t)(c >> 32)};
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {

@@ -174,15 +174,20 @@ struct FusedArgs {
     // for the launch, appends their finished episodes (headers from e.hring,
     // records from the lane rings) to this ticket's output at offsets from one
     // 64-bit atomic (episodes << 32 | records) and sets the lanes' harvested
-    // marks; the last workgroup to finish publishes the totals {episodes,
-    // records, error flags, episodes} to hv_info / hv_hinfo and zeroes the next
-    // output's counter. hv_hdr null: no harvest in this launch.
+    // marks; the last workgroup to finish moves the engine's error flags into
+    // this output's accumulator (atomic exchange with 0, so the flags of the
+    // launches since the previous ticket belong to this ticket alone), publishes
+    // the totals {episodes, records, error flags, episodes} to hv_info /
+    // hv_hinfo and zeroes the next output's counter and flags. hv_hdr null: no
+    // harvest in this launch.
     uint32_t* hv_hdr;            // [ep cap][EP_WORDS]
     uint32_t* hv_rec;            // [L * R][REC_WORDS]
     int hv_ep_cap;               // headers the output holds
     long long hv_rec_cap;        // records the output holds (L x R)
     unsigned long long* hv_ctr;  // this output's running totals
     unsigned long long* hv_next; // the next output's (zeroed by the last workgroup)
+    unsigned long long* hv_flags;       // this output's accumulated error flags
+    unsigned long long* hv_next_flags;  // the next output's (zeroed by the last workgroup)
     uint32_t* hv_info;           // [4] device
     uint32_t* hv_hinfo;          // [4] host-mapped
     unsigned long long* done_ctr;   // finished workgroups of the launch (the last one zeroes it)
@@ -214,6 +219,7 @@ hipError_t bgx_launch_validate(const uint8_t* boards, const uint8_t* player, con
                                unsigned* flags, hipStream_t stream);
 hipError_t bgx_launch_encode(const uint8_t* boards, const uint8_t* player, int n, float* out,
                              int layout, hipStream_t stream);
+hipError_t bgx_launch_encode_packed(const uint32_t* packed, int n, float* out, int layout, hipStream_t stream);
 hipError_t bgx_launch_value_f32(const float* x, int n, const float* W1, const float* b1,
                                 const float* w2, float b2, float* out, hipStream_t stream);
 hipError_t bgx_launch_pack(const uint8_t* boards, const uint8_t* player, int n, uint32_t* out,
@@ -233,9 +239,11 @@ hipError_t bgx_launch_td0(const bgx::TrainArgs* args, hipStream_t stream);
 hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* offsets, uint32_t* info, uint32_t* hinfo,
                                    hipStream_t stream);
 // in-kernel harvest bookkeeping when no fused launch ran since the last ticket:
-// publish the (empty) totals of ctr and zero the next output's counter
-hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next, const unsigned* err_flags,
-                                    uint32_t* info, uint32_t* hinfo, hipStream_t stream);
+// publish the (empty) totals of ctr with the accumulated error flags (the
+// engine's flags moved in) and zero the next output's counter and flags
+hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next, unsigned long long* flags,
+                                    unsigned long long* next_flags, unsigned* err_flags, uint32_t* info,
+                                    uint32_t* hinfo, hipStream_t stream);
 hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
                                      uint32_t* hout, uint32_t* out, hipStream_t stream);
 }

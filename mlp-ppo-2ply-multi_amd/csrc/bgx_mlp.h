@@ -192,8 +192,9 @@ BGX_DEV void mlp_item2(const uint4* wf, const uint4* lut, const float* w2s, floa
 // constant offsets below 64 KB; the asm hides the bases from the compiler,
 // which would otherwise fold them into one base plus an address add per read
 // (the fragments sit past the 64 KB an immediate offset reaches).
+template <bool STAMP = false>
 BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, float fs, uint4 bx, uint4 by,
-                        uint32_t kmask) {
+                        uint32_t kmask, unsigned long long* stamp = nullptr) {
     const int lane = (int)(threadIdx.x & 63);
     const int h = lane >> 5;
     lds_u4p wfh = (lds_u4p)(wf + lane);
@@ -220,6 +221,7 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
             }
         }
     }
+    if (STAMP) *stamp = wall_clock64();   // development (BGX_FUSED_PROF): the MFMA chain issued
     float v = 0.0f;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {

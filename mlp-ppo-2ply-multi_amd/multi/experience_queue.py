@@ -6,7 +6,7 @@ bulk path: a worker calls put_records(headers, records)
 once per harvest with the engine's compact records (EP_WORDS / REC_WORDS
 uint32 words per episode / experience); they go through a shared-memory ring
 (multi/shm_ring.py) instead of one pickle per episode, and get() decodes a
-whole message at once on the GPU (bgx_unpack + bgx_encode for the 198-d
+whole message at once on the GPU (bgx_unpack + bgx_encode_packed for the 198-d
 observations) before handing out Episodes one at a time, so src/main.py's
 `q.get(timeout=1)` loop runs unchanged.
 

@@ -6,8 +6,11 @@ given (gpus_for_worker: GPU g goes to worker g mod 7, so the reference's
 hard-coded 7 workers cover all 8 GPUs of a node — worker 0 drives GPUs 0 and 7;
 workers without a GPU return immediately), stepping thousands of lanes per
 GPU and putting every finished Episode on the queue exactly as
-play_episode/run do (worker.py:47-76). Parameters are re-read when the
-version advances (worker.py:66-76), at every harvest.
+play_episode/run do (worker.py:47-76). Each cycle queues the next launch and
+its harvest before the host reads the previous harvest (harvest_enqueue /
+harvest_fetch), so the GPUs keep stepping while the host copies and queues.
+Parameters are re-read when the version advances (worker.py:66-76), at every
+harvest.
 
 Knobs (environment): BGX_WORKERS (7: main.py:86's worker count),
 BGX_GPU_MAP (explicit GPUs per worker id: "0;1;2;3;4;5;6,7" = worker 6 drives
@@ -68,6 +71,7 @@ class Worker:
         self.max_pending = _env_int("BGX_MAX_PENDING", 2000)
         self.engines = []
         self.engine = None   # the first GPU's engine
+        self._pending = []   # the engines' harvest tickets of the launch in flight
 
     def _ensure_engine(self):
         """One engine per GPU of this worker: global lanes [g * lanes, (g + 1) *
@@ -94,30 +98,45 @@ class Worker:
             self.current_version = new_version
 
     def _step_all(self, steps):
+        """One pipelined cycle over this worker's engines: every engine's next
+        launch and its harvest ticket are queued first (the GPUs step
+        concurrently), then the PREVIOUS cycle's tickets are fetched, so the
+        host decodes / copies a harvest while the next launch runs and an
+        engine never waits for the host between launches (the reference's loop,
+        worker.py:47-76, plays one episode at a time). The harvests returned
+        are views into the engines' buffers, valid until the next cycle
+        queues its tickets; the first cycle returns none."""
         engines = self._ensure_engine()
-        for e in engines:   # asynchronous: the GPUs step concurrently
-            with torch.cuda.device(e.device):
-                e.step(steps or self.steps_per_harvest)
-        harvests = []
+        tickets = []
         for e in engines:
             with torch.cuda.device(e.device):
-                harvests.append(e.harvest())
+                e.step(steps or self.steps_per_harvest)
+                tickets.append(e.harvest_enqueue())
+        harvests = []
+        for e, t in zip(engines, self._pending):
+            with torch.cuda.device(e.device):
+                harvests.append(e.harvest_fetch(t))
+        self._pending = tickets
         return harvests
 
     def play_episodes(self, steps=None):
-        """Advance all lanes and return the Episodes that finished (already to_numpy()'d)."""
+        """Advance all lanes one launch and return the Episodes of the previous
+        launch's harvest (already to_numpy()'d)."""
         out = []
         for h in self._step_all(steps):
             out += to_episodes(h, Episode, Experience, Player)
         return out
 
     def harvest_records(self, steps=None):
-        """Advance all lanes; return the finished episodes as compact host arrays
-        (headers uint32 [n, 16], records uint32 [m, 12]) for the bulk queue path
-        (each episode's records contiguous, in header order, GPU by GPU)."""
+        """Advance all lanes one launch; return the previous launch's finished
+        episodes as compact host arrays (headers uint32 [n, 16], records
+        uint32 [m, 12]) for the bulk queue path (each episode's records
+        contiguous, in header order, GPU by GPU)."""
         hs = self._step_all(steps)
         hdr = [h.headers.cpu().numpy().view(np.uint32) for h in hs]
         rec = [h.records.cpu().numpy().view(np.uint32) for h in hs]
+        if not hs:
+            return np.zeros((0, 16), np.uint32), np.zeros((0, 12), np.uint32)
         if len(hs) == 1:
             return hdr[0], rec[0]
         return np.concatenate(hdr), np.concatenate(rec)
@@ -130,7 +149,9 @@ class Worker:
         bulk = hasattr(self.experience_queue, "put_records") and os.environ.get("BGX_BULK", "1") != "0"
         while True:
             if bulk:
-                self.experience_queue.put_records(*self.harvest_records())
+                hdr, rec = self.harvest_records()
+                if hdr.shape[0]:
+                    self.experience_queue.put_records(hdr, rec)
             else:
                 for episode in self.play_episodes():
                     self.experience_queue.put(episode)

@@ -430,13 +430,21 @@ void bgref_encode(const uint8_t* b, int player, int layout, float* f) {
 
 void bgref_value(const float* W1, const float* b1, const float* w2, const float* b2,
                  const float* x, int n, double* out) {
+    /* fp64 sums in feature order over the nonzero features only: a zero
+     * feature adds an exact (+-)0 to the running sum, so skipping it leaves
+     * every h bit-identical to the dense loop (a live row has ~28 nonzeros of
+     * 198, which makes the 2-ply checks ~7x cheaper) */
+    int nz[BGREF_NFEAT];
     for (int r = 0; r < n; ++r) {
         const float* xr = x + (size_t)r * BGREF_NFEAT;
+        int m = 0;
+        for (int k = 0; k < BGREF_NFEAT; ++k)
+            if (xr[k] != 0.0f) nz[m++] = k;
         double v = b2[0];
         for (int j = 0; j < BGREF_HIDDEN; ++j) {
             double h = b1[j];
             const float* w = W1 + (size_t)j * BGREF_NFEAT;
-            for (int k = 0; k < BGREF_NFEAT; ++k) h += (double)w[k] * (double)xr[k];
+            for (int q = 0; q < m; ++q) h += (double)w[nz[q]] * (double)xr[nz[q]];
             v += (double)w2[j] * (1.0 / (1.0 + exp(-h)));
         }
         out[r] = v;

@@ -44,7 +44,7 @@ def test_ctypes_table_covers_header(built):
 def test_loads_without_gpu_and_reports_version(built):
     import bgx
     L = bgx.lib()
-    assert L.bgx_abi_version() == 7
+    assert L.bgx_abi_version() == 8
     assert L.bgx_last_error() is not None
 
 
@@ -64,6 +64,8 @@ def test_argument_errors_cross_abi_as_codes(built):
     assert L.bgx_movegen(None, None, None, -1, None, None, 0, None) == -1
     assert b"n=-1" in L.bgx_last_error()
     assert L.bgx_encode(None, None, 5, None, 7, None) == -1
+    assert L.bgx_encode_packed(None, 5, None, 3, None) == -1
+    assert L.bgx_encode_packed(None, 5, None, 0, None) == -1   # null pointers, no device touched
     assert L.bgx_step(None, 1, None) == -1
 
 

@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -177,19 +178,46 @@ def test_gloo_world3_host_gather():
             np.testing.assert_array_equal(rec.reshape(-1), np.arange(2 * ne * 12) + 100 * seq)
 
 
-def test_host_gather_checks_shm_capacity(tmp_path):
-    """bench.py's host gather first checks that every rank's segment (a header
-    + two slots, page-locked in full) fits the node's shared-memory filesystem
-    and otherwise falls back to the RCCL gather: a tmpfs would accept the
-    segment and fail only when the copies touch its pages."""
+def test_host_gather_segments_do_not_use_dev_shm():
+    """bench.py's host gather keeps its segments in anonymous memory files
+    (memfd), so the path --gpus 8 takes does not depend on /dev/shm's size (a
+    container's tmpfs is often 64 MB; a rank's segment at 8,192 lanes is
+    ~0.5 GB): a segment larger than /dev/shm's free space is created and its
+    last page written, and nothing appears under /dev/shm."""
     import sys
     from conftest import PKG
     sys.path.insert(0, PKG)
     from bgx import hostgather
     slot = hostgather.slot_bytes_for(8192, 300)
     assert slot >= 8192 * 600 * 48   # a record per lane-step since the last harvest + the open episodes
-    st = os.statvfs(str(tmp_path))
+    st = os.statvfs("/dev/shm")
     free = st.f_bavail * st.f_frsize
-    assert hostgather.shm_fits(1, 4096, path=str(tmp_path))
-    assert not hostgather.shm_fits(8, free, path=str(tmp_path))
-    assert not hostgather.shm_fits(2, slot, path=str(tmp_path / "missing"))
+    before = set(os.listdir("/dev/shm"))
+    g = hostgather.HostGather(1, 2, hostgather.make_tag(), slot_bytes=free // 2 + (1 << 20))
+    try:
+        assert g._mine.size > free
+        g._mine.buf[g._mine.size - 1] = 7            # a sparse file: only the touched page is backed
+        assert g._mine.buf[g._mine.size - 1] == 7
+        assert not any("bgx_hg" in n for n in set(os.listdir("/dev/shm")) - before)
+    finally:
+        g.close()
+
+
+def test_host_gather_oversized_harvest_keeps_batch_numbers():
+    """A harvest larger than the slot raises before the batch number moves
+    (ADVICE r3): the rank can still publish the batch dst waits for."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    from bgx import hostgather
+    from bgx.engine import Harvest
+    g = hostgather.HostGather(1, 2, hostgather.make_tag(), slot_bytes=4096)
+    try:
+        big = Harvest(torch.zeros((1, 16), dtype=torch.int32), torch.zeros((100, 12), dtype=torch.int32))
+        with pytest.raises(ValueError):
+            g.publish(big)
+        assert g.seq == 0
+        p = g.publish(Harvest(torch.ones((1, 16), dtype=torch.int32), torch.ones((2, 12), dtype=torch.int32)))
+        assert p.wait() == 1 and int(g.ctrl[1][0]) == 1
+    finally:
+        g.close()

@@ -121,7 +121,14 @@ def _hg_rank(rank, world, port, L, steps, out):
             parts[0] = (h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32))
             got.append(parts)
         else:
-            g.publish(h).wait()      # DMA-engine copy into the shared segment, then publish
+            # DMA-engine copy into the segment; the Harvest is dropped at once and
+            # its blocks are asked for again before the copy is waited for: the
+            # Pending keeps them, so rank 0 still gets intact records
+            p = g.publish(h)
+            del h
+            junk = [torch.full((1 << 20,), -1, dtype=torch.int32, device="cuda") for _ in range(16)]
+            p.wait()
+            del junk
     e.close()
     if rank == 0:
         out.put(got)
@@ -131,9 +138,11 @@ def _hg_rank(rank, world, port, L, steps, out):
 
 
 def test_host_gather_world2_real_harvests(weights_seed0):
-    """bench.py --gather host with real engines: two ranks on cuda:0, rank 1's
-    harvests reach rank 0 through page-locked shared memory by the copy
-    engines (bgx_copy_async); merged == one Engine over both lane blocks."""
+    """bench.py --gather host (the path bench.py --gpus N takes, whatever
+    /dev/shm holds) with real engines: two ranks on cuda:0, rank 1's harvests
+    reach rank 0 through page-locked anonymous shared memory (memfd segments
+    handed over by SCM_RIGHTS) by the SDMA engines (bgx_dma_copy_d2h); merged
+    == one Engine over both lane blocks."""
     from bgx import Engine
     from bgx.records import episode_bounds
     L, steps = 128, 240

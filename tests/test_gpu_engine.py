@@ -467,19 +467,77 @@ def test_fused_in_kernel_harvest_slots(weights_seed0):
 
 
 def test_fused_harvest_past_capacity_is_an_error(weights_seed0):
-    """Several fused launches without a harvest append more finished episodes
-    than a small output holds (ep_cap = 64 headers): the in-kernel harvest
-    copies nothing past the output and the fetch reports BGX_E_STATE; the
-    engine keeps running and harvests normally afterwards."""
+    """Several fused launches without a harvest finish more episodes than a
+    small output holds (ep_cap = 64 headers): a workgroup whose episodes do
+    not fit copies nothing and keeps them in its lanes' rings for the next
+    ticket; once the rings overflow (ring = 512) the episodes are lost and the
+    fetch reports BGX_E_CAPACITY (flag 8). Only the overflowing lanes are
+    dropped; the engine keeps running and harvests normally afterwards."""
     from bgx import BgxError
     e = _engine(weights_seed0, lanes=64, seed=5, ply=1, fused=True, ep_cap=64, ring=512)
     for _ in range(5):
         e.step(200)
-    with pytest.raises(BgxError):
+    with pytest.raises(BgxError, match=r"\(-3\).*flags 0x8"):
         e.harvest()
     e.step(40)
     h = e.harvest()
     assert 0 < h.n_episodes <= 64
+    e.sync()
+    e.close()
+
+
+def test_fused_over_capacity_episodes_wait_for_the_next_ticket(weights_seed0):
+    """A launch whose finished episodes exceed the ticket's output (ep_cap)
+    keeps the groups that do not fit in the rings; the next ticket delivers
+    them. Over both tickets every (lane, episode) equals an engine with room
+    for all, and nothing is reported lost."""
+    ref = _engine(weights_seed0, lanes=128, seed=8, ply=1, fused=True)
+    ref.step(200)
+    h = ref.harvest()
+    from bgx.episodes import decode_records
+    hdr = h.headers.cpu().numpy().view(np.uint32)
+    want = _by_episode([hdr], [decode_records(hdr, h.records)])
+    ref.close()
+    e = _engine(weights_seed0, lanes=128, seed=8, ply=1, fused=True, ep_cap=150)
+    e.step(200)                 # ~280 episodes finish; the output holds 150 headers
+    hs, rs = [], []
+    for _ in range(3):          # the held groups come with the following (empty-launch) tickets
+        h = e.harvest()
+        hdr = h.headers.cpu().numpy().view(np.uint32)
+        assert hdr.shape[0] <= 150
+        hs.append(hdr)
+        rs.append(decode_records(hdr, h.records))
+        e.step(1)
+    e.sync()
+    e.close()
+    got = _by_episode(hs, rs)
+    assert len(want) > 150
+    assert want.keys() <= got.keys()
+    for key in want:
+        np.testing.assert_array_equal(got[key][0], want[key][0], err_msg=str(key))
+        for f in want[key][1]:
+            np.testing.assert_array_equal(got[key][1][f], want[key][1][f], err_msg=f"{key} {f}")
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_fetch_reports_only_its_tickets_flags(weights_seed0, fused):
+    """Error flags belong to the ticket whose launches raised them:
+    with the next launch already queued behind a failing ticket, fetching the
+    failing ticket reports its flags, and the next ticket (whose launch was in
+    flight during that fetch) reports none."""
+    from bgx import BgxError
+    e = _engine(weights_seed0, lanes=64, seed=5, ply=1, fused=fused, ring=512)
+    for _ in range(4):
+        e.step(200)             # no harvest: the 512-slot rings overflow (flag 8)
+    t0 = e.harvest_enqueue()
+    e.step(40)                  # in flight while t0 is fetched
+    t1 = e.harvest_enqueue()
+    with pytest.raises(BgxError, match="flags 0x8"):
+        e.harvest_fetch(t0)
+    h = e.harvest_fetch(t1)
+    assert h.n_episodes >= 0
+    e.step(40)
+    e.harvest()
     e.sync()
     e.close()
 

@@ -1,0 +1,182 @@
+"""Parity at the benchmarked scale and run-to-run reproducibility.
+
+* The bench's exact 1-ply shape (bench.py run_engine): Engine(8,192 lanes,
+  balance=True) -- the FL = 32 fused kernel, one 32-lane group per CU, the
+  balanced lane-step budget, the tier-1 expansion carried across launches, the
+  in-kernel harvest into three rotating slots -- driven as bench.py drives
+  it: 300 desync steps, then two 300-step launches, each harvest queued
+  behind its launch (harvest_enqueue) and fetched while the next launch runs.
+  Every header of every harvest is checked for the episode bookkeeping
+  (each lane's episodes 0, 1, 2, ... exactly once, contiguous first records,
+  lengths, terminal flags), and a seeded random sample of whole episodes
+  holding >= 20,000 records is replayed transition by transition through the
+  oracle (test_gpu_engine._check_transitions: afterstate, V(s) / V(a),
+  reward, done, win type, shaping, observations). Reference loop:
+  src/multi/worker.py:101-162 over backgammon_env.py:130-308.
+* 2-ply K = all at 4,096 lanes (configs[2]'s lane count), greedy: >= 2,000
+  sampled decisions equal the oracle's argmax of 1.0 * V - 0.9 * W over every
+  candidate (two_ply.py:44-150).
+* The same seed twice in one process gives identical records for 2-ply
+  reference-sampled (reply_sample = 50, two_ply.py:119-121) and K = all
+  (DESIGN.md section 4 argues why no kernel reads a reply row outside its
+  job's range; this is the run-level check).
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from test_gpu_engine import _by_episode, _check_transitions, _collect, _same_runs
+
+pytestmark = pytest.mark.gpu
+V_TOL = 1e-5
+
+
+def _engine(weights, **kw):
+    from bgx import Engine
+    e = Engine(**kw)
+    e.set_weights(weights, temperature=1.5, version=1)
+    return e
+
+
+def _bench_run(e, n, chunk, out):
+    """bench.py run_engine's run(): launch, queue its harvest, fetch the
+    previous one while this launch runs; harvests copied to host as fetched."""
+    left, pending = n, None
+
+    def take(t):
+        h = e.harvest_fetch(t)
+        out.append((h.headers.cpu().numpy().view(np.uint32).copy(), h.records.cpu().numpy().view(np.uint32).copy()))
+
+    while left > 0:
+        k = min(chunk, left)
+        e.step(k)
+        t = e.harvest_enqueue()
+        if pending is not None:
+            take(pending)
+        pending = t
+        left -= k
+    take(pending)
+
+
+def _check_headers(harvests, lanes, max_steps=300):
+    """Episode bookkeeping over every harvest: lanes in range, each lane's
+    episode numbers 0, 1, 2, ... exactly once and in order across harvests,
+    each episode's records contiguous after its predecessor's, lengths and
+    terminal flags consistent. Returns the number of episodes."""
+    from bgx.records import fields
+    nxt_ep = np.zeros(lanes, np.int64)
+    nxt_rec = np.zeros(lanes, np.int64)
+    n_eps = 0
+    for hdr, rec in harvests:
+        assert rec.shape[0] == int(hdr[:, 3].astype(np.int64).sum())
+        f = fields(rec)
+        o = 0
+        for row in hdr:
+            lane, ep, first, n, steps = (int(x) for x in row[:5])
+            assert 0 <= lane < lanes
+            assert ep == nxt_ep[lane], (lane, ep, nxt_ep[lane])
+            assert first == nxt_rec[lane], (lane, ep, first, nxt_rec[lane])
+            nxt_ep[lane] += 1
+            nxt_rec[lane] += n
+            assert 1 <= n <= steps <= max_steps
+            st = f["step"][o:o + n]
+            assert np.all(np.diff(st) >= 1) and st[0] >= 0 and st[-1] < steps
+            done = f["done"][o:o + n]
+            assert not done[:-1].any()
+            if steps < max_steps:   # a game that ended before the step cap ended on a win
+                assert done[-1] and st[-1] == steps - 1 and f["win_type"][o + n - 1] > 0
+                assert int(row[5]) & 0xFF == int(f["win_type"][o + n - 1])
+            assert not f["win_type"][o:o + n - 1].any()
+            o += n
+            n_eps += 1
+    return n_eps
+
+
+def _subset(hdr, rec, pick):
+    """Headers `pick` (indices into hdr) and their records, concatenated."""
+    offs = np.concatenate([[0], np.cumsum(hdr[:, 3].astype(np.int64))])
+    sub = hdr[pick]
+    parts = [rec[offs[i]:offs[i + 1]] for i in pick]
+    return sub, np.concatenate(parts) if parts else rec[:0]
+
+
+def test_bench_shape_1ply_matches_oracle(weights_seed0):
+    import torch
+    from bgx.episodes import decode_records
+    lanes, chunk = 8192, 300
+    e = _engine(weights_seed0, lanes=lanes, seed=0, ply=1, balance=True)
+    assert e.fused
+    harvests = []
+    _bench_run(e, 300, chunk, harvests)        # bench.py --desync-steps
+    s0 = e.stats()
+    _bench_run(e, 600, chunk, harvests)        # two 300-step launches, pipelined harvests
+    s1 = e.stats()
+    e.close()
+    groups = lanes // 32
+    done = s1["env_steps"] - s0["env_steps"]
+    # the budget, plus less than one 32-lane workgroup-step per workgroup and launch
+    assert lanes * 600 <= done < lanes * 600 + 2 * groups * 32, done
+    n_eps = _check_headers(harvests, lanes)
+    assert n_eps > 20000
+    # a seeded random sample of whole episodes, >= 20,000 records, through the oracle
+    rng = np.random.default_rng(2026)
+    checked = 0
+    for hdr, rec in harvests:
+        order = rng.permutation(hdr.shape[0])
+        lens = hdr[order, 3].astype(np.int64)
+        take = order[:int(np.searchsorted(np.cumsum(lens), 7000)) + 1]
+        sub_h, sub_r = _subset(hdr, rec, np.sort(take))
+        d = decode_records(sub_h, torch.from_numpy(sub_r.view(np.int32)).cuda())
+        checked += _check_transitions(weights_seed0, [sub_h], [d], 1)
+    assert checked >= 20000, checked
+
+
+def _kall_scores(w, board, mover, d0, d1):
+    """two_ply.py:44-90 with every candidate: 1.0 * V - 0.9 * W (oracle, fp64)."""
+    cnt, res, _ = orc.movegen(board, mover, d0, d1)
+    m = min(cnt, 500)
+    v = orc.value(w, orc.encode_many(res[:m], [mover] * m))
+    W = np.array([orc.two_ply_response(w, res[c], 1 - mover) for c in range(m)])
+    return 1.0 * v - 0.9 * W
+
+
+def test_kall_4096_lanes_greedy_is_oracle_argmax(weights_seed0):
+    from bgx.episodes import decode_records
+    lanes = 4096
+    e = _engine(weights_seed0, lanes=lanes, seed=19, ply=2, k_top=0, greedy=True)
+    e.step(150)
+    h = e.harvest()
+    hdr = h.headers.cpu().numpy().view(np.uint32)
+    d = decode_records(hdr, h.records)
+    e.close()
+    m = d["action"].shape[0]
+    assert m > 20000
+    rng = np.random.default_rng(7)
+    ks = rng.choice(m, 2000, replace=False)
+
+    def one(k):
+        s = _kall_scores(weights_seed0, d["before"][k], int(d["mover"][k]), *d["dice"][k])
+        a = int(d["action"][k])
+        return a, float(s[a]), float(s.max()), len(s)
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:   # ctypes drops the GIL
+        res = list(ex.map(one, ks))
+    for k, (a, sa, smax, n) in zip(ks, res):
+        assert 0 <= a < n
+        assert sa >= smax - 2 * V_TOL, (int(k), a, sa, smax)
+    assert len(res) == 2000
+
+
+@pytest.mark.parametrize("k_top,sample", [(4, 50), (0, 0)])
+def test_2ply_same_seed_same_records(weights_seed0, k_top, sample):
+    """Two engines with the same seed, one after the other in one process:
+    identical episodes and records (2-ply reference-sampled and K = all)."""
+    runs = []
+    for _ in range(2):
+        e = _engine(weights_seed0, lanes=256, seed=41, ply=2, k_top=k_top, reply_sample=sample)
+        runs.append(_by_episode(*_collect(e, 90 if k_top else 60, chunk=30)))
+        e.close()
+    _same_runs(*runs)
