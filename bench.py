@@ -115,13 +115,13 @@ def sum_over_ranks(x, world):
 
 
 def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_every, timing, timing_steps=0,
-               desync=0):
+               desync=0, seed=None):
     from bgx import Engine
     from bgx import dist as bdist
     w = load_weights()
     if world > 1:
         w = bdist.broadcast_weights(w)
-    eng = Engine(lanes=lanes, seed=args.seed, ply=ply, k_top=k_top, lane_base=rank * lanes,
+    eng = Engine(lanes=lanes, seed=args.seed if seed is None else seed, ply=ply, k_top=k_top, lane_base=rank * lanes,
                  fused=not args.no_fused, balance=not args.no_balance)
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
@@ -413,8 +413,13 @@ def spawn_ranks(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps of the headline leg (the driver passes it: one run at --seed). Without it, "
+                         "SURVEY 8d's protocol: every leg over seeds 0-4, each with a timed window of >= "
+                         "--window-s seconds, the median reported")
     ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--window-s", type=float, default=10.0, help="protocol mode: timed seconds per leg and seed")
+    ap.add_argument("--seeds", type=int, default=5, help="protocol mode: seeds 0..n-1")
     ap.add_argument("--lanes", type=int, default=8192,
                     help="lanes per GPU (8,192: configs[3]/[4]'s 65,536 lanes over 8 GPUs)")
     ap.add_argument("--ply", type=int, default=1)
@@ -471,14 +476,14 @@ def main():
 
     world, rank, local = init_dist()
 
-    def leg(ply, k_top, lanes, steps, warmup, timing_steps, name, desync=None):
+    def leg(ply, k_top, lanes, steps, warmup, timing_steps, name, desync=None, seed=None):
         desync = args.desync_steps if desync is None else desync
         el_, d_, tm_, dtm_, gathered_ = run_engine(args, world, rank, ply, k_top, lanes, steps, warmup,
-                                                   args.harvest_every, timing=True, timing_steps=timing_steps,
-                                                   desync=desync)
+                                                   args.harvest_every, timing=timing_steps > 0,
+                                                   timing_steps=timing_steps, desync=desync, seed=seed)
         el_ = max_over_ranks(el_, world)
         per_rank = [int(x) for x in all_ranks(d_["env_steps"], world)]
-        roof_, kern_ = roofline_for(dtm_, tm_, name)
+        roof_, kern_ = roofline_for(dtm_, tm_, name) if timing_steps > 0 else (None, None)
         out_ = {"value": sum(per_rank) / el_, "unit": "env_steps/s", "steps": steps, "lanes_per_gpu": lanes,
                 "ms_per_step": el_ / steps * 1e3, "env_steps_per_rank": per_rank,
                 "decisions_per_s": sum_over_ranks(d_["decisions"], world) / el_,
@@ -486,25 +491,62 @@ def main():
                 "value_rows_per_s": sum_over_ranks(d_["value_rows"], world) / el_,
                 "movegen_jobs_per_s": sum_over_ranks(d_["movegen_jobs"], world) / el_,
                 "fallback_jobs": int(sum_over_ranks(d_["fallback_jobs"], world)),
-                "roofline": roof_, "kernels": kern_, "desync_steps": desync}
+                "roofline": roof_, "kernels": kern_, "desync_steps": desync,
+                "seed": args.seed if seed is None else seed}
         if world > 1:
             out_["gathered_episodes"], out_["gathered_records"] = gathered_
+        if rank == 0:   # progress on stderr (the JSON line is stdout's only line)
+            print(f"[bench] {name} lanes={lanes} seed={out_['seed']} steps={steps}: {out_['value'] / 1e6:.2f} M env "
+                  f"steps/s, {out_['ms_per_step']:.4f} ms/step", file=sys.stderr, flush=True)
         return out_, d_
 
-    head, d = leg(args.ply, args.k_top, args.lanes, args.steps, args.warmup, min(args.steps, args.timing_steps),
-                  "1ply" if args.ply == 1 else ("2ply_k4" if args.k_top == 4 else "2ply_kall"))
+    def protocol(ply, k_top, lanes, warmup, timing_steps, name, short_steps):
+        """seeds 0..n-1, each a fresh engine with a timed window of
+        >= --window-s seconds (steps sized from a short calibration run of
+        seed 0), the median by value reported with every seed's figures."""
+        cal, _ = leg(ply, k_top, lanes, short_steps, warmup, 0, name, seed=0)
+        per = args.harvest_every
+        steps = max(short_steps, -(-int(args.window_s * 1e3 / cal["ms_per_step"]) // per) * per)
+        runs = []
+        for sd in range(args.seeds):
+            r, d_ = leg(ply, k_top, lanes, steps, warmup, timing_steps if sd == 0 else 0, name, seed=sd)
+            runs.append((r, d_))
+        order = sorted(range(len(runs)), key=lambda i: runs[i][0]["value"])
+        med, dmed = runs[order[len(runs) // 2]]
+        med = dict(med)
+        med["roofline"], med["kernels"] = runs[0][0]["roofline"], runs[0][0]["kernels"]   # seed 0's timing pass
+        med["protocol"] = {"seeds": [r["seed"] for r, _ in runs], "values": [r["value"] for r, _ in runs],
+                           "ms_per_step": [r["ms_per_step"] for r, _ in runs], "steps_per_seed": steps,
+                           "window_s": [r["ms_per_step"] * steps * 1e-3 for r, _ in runs],
+                           "median_seed": med["seed"], "calibration_steps": short_steps}
+        return med, dmed
+
+    proto = args.steps is None
+    head_name = "1ply" if args.ply == 1 else ("2ply_k4" if args.k_top == 4 else "2ply_kall")
+    if proto:
+        head, d = protocol(args.ply, args.k_top, args.lanes, args.warmup, args.timing_steps, head_name, 1200)
+        args.steps = head["steps"]
+    else:
+        head, d = leg(args.ply, args.k_top, args.lanes, args.steps, args.warmup, min(args.steps, args.timing_steps),
+                      head_name)
     extra = {}
     if args.ply == 1 and args.two_ply_steps > 0:
-        extra["two_ply_k4"], _ = leg(2, 4, args.lanes, args.two_ply_steps, 20,
-                                     min(args.two_ply_steps, args.timing_steps, 50), "2ply_k4")
+        extra["two_ply_k4"], _ = (protocol(2, 4, args.lanes, 20, min(args.timing_steps, 50), "2ply_k4", 100)
+                                  if proto else
+                                  leg(2, 4, args.lanes, args.two_ply_steps, 20,
+                                      min(args.two_ply_steps, args.timing_steps, 50), "2ply_k4"))
     if args.ply == 1 and args.kall_steps > 0:
-        extra["two_ply_kall"], d3 = leg(2, 0, args.lanes, args.kall_steps, 5,
-                                        min(args.kall_steps, args.timing_steps, 10), "2ply_kall")
+        extra["two_ply_kall"], d3 = (protocol(2, 0, args.lanes, 5, min(args.timing_steps, 10), "2ply_kall", 20)
+                                     if proto else
+                                     leg(2, 0, args.lanes, args.kall_steps, 5,
+                                         min(args.kall_steps, args.timing_steps, 10), "2ply_kall"))
         extra["two_ply_kall"]["reply_boards_per_decision"] = \
             (d3["value_rows"] - 2 * d3["env_steps"]) / max(1, d3["decisions"])
     if args.ply == 1 and world == 1 and args.config1_steps > 0 and args.lanes != 4096:
-        c1, _ = leg(1, 4, 4096, args.config1_steps, 100, min(args.config1_steps, args.timing_steps), "1ply")
-        extra["configs1_4096_lanes"] = {k: c1[k] for k in ("value", "unit", "steps", "ms_per_step", "roofline")}
+        c1, _ = (protocol(1, 4, 4096, 100, min(args.config1_steps, args.timing_steps), "1ply", 600) if proto else
+                 leg(1, 4, 4096, args.config1_steps, 100, min(args.config1_steps, args.timing_steps), "1ply"))
+        extra["configs1_4096_lanes"] = {k: c1[k] for k in ("value", "unit", "steps", "ms_per_step", "roofline")
+                                        + (("protocol",) if proto else ())}
 
     if rank == 0:
         line = {
@@ -530,6 +572,10 @@ def main():
             "decisions_per_s": head["decisions_per_s"], "episodes_per_s": head["episodes_per_s"],
             "value_rows_per_s": head["value_rows_per_s"], "fallback_jobs": head["fallback_jobs"],
             "roofline": head["roofline"], "kernels": head["kernels"], "cpu_baseline": cpu,
+            "seed": head["seed"], "protocol": head.get("protocol"),
+            "episodes_per_s_note": "device-side: episodes finished and harvested on the GPU per second"
+                                   + (" (at N = 1 nothing is moved off the device inside the timed region)"
+                                      if world == 1 else ""),
         }
         if world > 1:
             line["gathered_episodes"], line["gathered_records"] = head["gathered_episodes"], head["gathered_records"]

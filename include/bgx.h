@@ -143,8 +143,10 @@ typedef struct bgx_config {
     int greedy;             /* 1: argmax of the scores instead of sampling (play_versus_ai.py:188-195,
                                torch.argmax: first maximum); the sampling uniform is still drawn */
     int fused;              /* 1-ply only, 1 (default): bgx_step runs as ONE persistent launch in which
-                               each 16-lane workgroup advances its lanes through all n_steps (movegen,
-                               MLP, select, step fused; same results as 0 = one launch per phase) */
+                               each workgroup (one per CU: 32 lanes on 12 waves when lanes >= 32 x CUs,
+                               else 16 lanes on 8 waves) advances its lanes through all n_steps
+                               (movegen, MLP, select, step fused; same results as 0 = one launch per
+                               phase) */
     int reply_sample;       /* 2-ply: 0 (default) = exact mode; 50 = the reference's random.sample of 50
                                replies for 1-1 / 2-2 / 3-3 (two_ply.py:119-121), keyed by seed + step */
     int balance;            /* fused 1-ply, lanes <= 32 x CUs: 1 = bgx_step(n) runs n x lanes lane-steps in
@@ -226,6 +228,15 @@ int bgx_harvest(bgx_engine* e, bgx_harvest_info* out, void* stream);
  * same. */
 int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream);
 int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out);
+/* Error flags (capacity overflows, a bounded wait) belong to a ticket: the
+ * device moves the flags raised by the steps since the previous ticket into
+ * that ticket's totals (an atomic exchange, in stream order), and
+ * bgx_harvest_fetch reports them for that ticket only; a launch in flight
+ * during the fetch is never affected. bgx_sync reports the flags raised since
+ * the last ticket. A fused engine's workgroup whose finished episodes do not
+ * fit the ticket's output copies nothing and keeps them in its lanes' rings
+ * for the next ticket (not an error); episodes are lost, and reported, only
+ * when a lane's ring is overwritten before they are harvested. */
 
 typedef struct bgx_stats {
     uint64_t env_steps;     /* lane steps (passes included) */
