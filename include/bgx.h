@@ -295,6 +295,17 @@ int bgx_copy_async(void* dst, const void* src, uint64_t bytes, int kind, void* s
 int bgx_dma_copy_d2h(void* h_dst, const void* d_src, uint64_t bytes, int device, uint64_t* ticket);
 int bgx_dma_wait(uint64_t ticket, int timeout_ms);
 
+/* The 2-ply reply expansion alone (the engine's and bgx_two_ply's reply
+ * launch, two_ply.py:114-133 before the value calls): for each of n candidate
+ * boards, the opponent's legal afterstates for all 21 DICE_ROLLS
+ * (two_ply.py:10-32), as packed boards (flag = the opponent) in d_out[cap][8];
+ * job i * 21 + r's records are rows d_off[j] .. d_off[j] + d_cnt[j] - 1
+ * (other rows are unused). Parity hook for the board-major reply kernel
+ * (BGX_REPLY_BM=0 selects the per-(board, roll) kernel); BGX_E_CAPACITY when
+ * cap is too small. */
+int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, uint32_t* d_out, int cap,
+                    int32_t* d_off, int32_t* d_cnt, void* stream);
+
 /* Convert between u8[52] boards and the engine's packed boards (device). */
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream);
 int bgx_unpack(const uint32_t* d_packed, int n, uint8_t* d_boards, void* stream);

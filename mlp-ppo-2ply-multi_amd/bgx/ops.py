@@ -85,6 +85,22 @@ def encode_packed(packed, layout: int = 0, stream=None):
     return out
 
 
+def reply_moves(boards, opponent, cap: int = 0, stream=None):
+    """The 2-ply reply expansion (include/bgx.h bgx_reply_moves): for each
+    candidate board, the opponent's afterstates for the 21 DICE_ROLLS.
+    Returns (rows int32 [cap, 8] packed, off int32 [n * 21], cnt int32 [n * 21])."""
+    boards, opponent = _u8(boards).view(-1, 52), _u8(opponent).view(-1)
+    require_cuda(boards, opponent)
+    n = boards.shape[0]
+    cap = cap or n * 21 * 64 + 4096
+    out = torch.empty((cap, 8), dtype=torch.int32, device=boards.device)
+    off = torch.empty((n * 21,), dtype=torch.int32, device=boards.device)
+    cnt = torch.empty((n * 21,), dtype=torch.int32, device=boards.device)
+    check(lib().bgx_reply_moves(ptr(boards), ptr(opponent), n, ptr(out), cap, ptr(off), ptr(cnt),
+                                stream_handle(stream)), "bgx_reply_moves")
+    return out, off, cnt
+
+
 def pack(boards, player, stream=None):
     boards, player = _u8(boards).view(-1, 52), _u8(player).view(-1)
     require_cuda(boards, player)

@@ -654,6 +654,70 @@ int bgx_dma_wait(uint64_t ticket, int timeout_ms) {
     });
 }
 
+int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, uint32_t* d_out, int cap,
+                    int32_t* d_off, int32_t* d_cnt, void* stream) {
+    return guarded("bgx_reply_moves", [&]() -> int {
+        if (n < 0 || cap < 0) return fail(BGX_E_ARG, "bgx_reply_moves: n=%d cap=%d", n, cap);
+        if (n == 0) return BGX_OK;
+        if (!d_boards || !d_opponent || !d_out || !d_off || !d_cnt) return fail(BGX_E_ARG, "bgx_reply_moves: null pointer");
+        DeviceScope ds(d_boards);
+        HIP_TRY(ds.err);
+        hipStream_t s = (hipStream_t)stream;
+        {
+            Lease L;
+            if (int rc = lease_scratch(s, L)) return rc;
+            if (int rc = require_domain("bgx_reply_moves", L.sc, d_boards, d_opponent, nullptr, n, s)) return rc;
+        }
+        uint8_t* mover = nullptr;
+        uint32_t *rows = nullptr, *ws = nullptr;
+        unsigned* ctr = nullptr;
+        int32_t* ovf = nullptr;
+        int rc = BGX_OK;
+        const int ws_waves = 64, ws_slots = 16384, ovf_cap = 1 << 16;
+        if (dalloc(&mover, n) || dalloc(&rows, (size_t)n * 8) || dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) ||
+            dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
+            rc = BGX_E_HIP;
+        if (!rc) {
+            std::vector<uint8_t> ho(n), hm(n);
+            if (hipMemcpy(ho.data(), d_opponent, n, hipMemcpyDeviceToHost) != hipSuccess) rc = BGX_E_HIP;
+            for (int i = 0; i < n; ++i) hm[i] = (uint8_t)(1 - (ho[i] & 1));   // the candidate's mover
+            if (!rc && hipMemcpy(mover, hm.data(), n, hipMemcpyHostToDevice) != hipSuccess) rc = BGX_E_HIP;
+        }
+        if (!rc && hipMemsetAsync(ctr, 0, 32, s) != hipSuccess) rc = BGX_E_HIP;
+        if (!rc && bgx_launch_pack(d_boards, mover, n, rows, s) != hipSuccess) rc = BGX_E_HIP;
+        if (!rc) {
+            bgx::MovegenArgs b{};
+            b.n_jobs = n * 21;
+            b.in_mode = bgx::IN_TWOPLY;
+            b.in_packed = rows;
+            b.out_mode = bgx::OUT_PACKED_FLAT;
+            b.out_packed = d_out;
+            b.flat_count = ctr;
+            b.flat_cap = cap;
+            b.flat_chunk = 256;
+            b.job_off = d_off;
+            b.job_cnt = d_cnt;
+            b.ovf_count = ctr + 2;
+            b.ovf_list = ovf;
+            b.ovf_cap = ovf_cap;
+            b.ws_global = ws;
+            b.ws_waves = ws_waves;
+            b.ws_slots = ws_slots;
+            b.ws_words_per_wave = (size_t)5 * ws_slots;
+            b.err_flags = ctr + 3;
+            if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
+        }
+        unsigned flags = 0;
+        if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
+            rc = BGX_E_HIP;
+        void* ps[] = {mover, rows, ctr, ovf, ws};
+        for (void* p : ps) hipFree(p);
+        if (rc) return fail(rc, "bgx_reply_moves: HIP failure");
+        if (flags) return fail(BGX_E_CAPACITY, "bgx_reply_moves: overflow flags 0x%x", flags);
+        return BGX_OK;
+    });
+}
+
 int bgx_pack(const uint8_t* d_boards, const uint8_t* d_player, int n, uint32_t* d_packed, void* stream) {
     return guarded("bgx_pack", [&]() -> int {
         if (n < 0) return fail(BGX_E_ARG, "bgx_pack: n=%d", n);

@@ -882,6 +882,193 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
     return nfin;
 }
 
+// ------------------------------------------------------------------ board-major replies (2-ply)
+// two_ply.py:114-133 expands every roll of every candidate. The per-(root,
+// roll) job above redoes the root analysis, its first-move lists and a
+// mostly idle 64-lane emission for each of the 21 rolls; here one wave runs
+// the 15 NON-DOUBLES rolls of a root together:
+//  * each lane holds one FIRST move (die d, source s1), dice descending in
+//    lane order; roll (H, L) takes its pass-0 parents (high die first) from
+//    the die-H lanes and its pass-1 parents from the die-L lanes, so in lane
+//    order a roll's pass-0 parents precede its pass-1 parents -- the
+//    reference's (pass, i, j) enumeration (handle_non_doubles,
+//    generate_all_moves.py:23-68);
+//  * a roll's children are expanded flat over its parent lanes (64 per
+//    round, flat_parent) and its records appended to one list for the root;
+//  * the root's records are written in one pass (all 64 lanes busy), and the
+//    15 jobs get their offsets inside that block.
+// Roots it applies to (the others return -1 and run as per-roll jobs):
+//  - rule mode (nd_by_rule: nothing on the bar, >= 3 mover checkers outside
+//    home): no node of the two-step tree is on the bar or bearing off; records
+//    are filtered by nd_first exactly as job_records' rule branch;
+//  - the mover on the bar: the only first move of a die is the bar entry; a
+//    child's moves are the normal moves of the entered board (bar 1: the
+//    entered checker is outside home, so no bear-off) or the second entry
+//    (bar >= 2). The two passes' plays are distinct except one board: with
+//    bar 1 the two chains (enter and move on with the other die) end on the
+//    same point and are the same board iff neither entry point held a blot;
+//    with bar >= 2 the two double entries are the same board. Every other
+//    pair differs in the mover's checkers (an addition at e_H = x + H would
+//    need a source x off the board). So a pass-1 play is dropped iff its key
+//    equals that pass-0 play's key; nothing else needs a table.
+// Keys (nd_key, the non-doubles record format) go to `list` roll-major, the
+// rolls in DICE_ROLLS order (two_ply.py:10-32) without the doubles; lane q of
+// `rcnt` = the record count of the q-th non-doubles roll. Returns the record
+// count, or -1 (not applicable, more than 64 first moves, or the list is full).
+constexpr int ND_ROLLS = 15;
+// index in the 21 DICE_ROLLS of the q-th non-doubles roll (the doubles sit at 0, 6, 11, 15, 18, 20)
+BGX_DEV int nd_roll_q21(int q) { return q + 1 + (q >= 5) + (q >= 9) + (q >= 12) + (q >= 14); }
+BGX_DEV int dbl_q21(int d) { return (d - 1) * 7 - ((d - 1) * d) / 2; }   // (d, d), d = 1..6
+
+template <int LISTCAP>
+BGX_DEV int board_nd_records(const Root& R, uint32_t* map, uint32_t* list, int& rcnt) {
+    const int l = lane_id();
+    const bool p0 = R.player == 0;
+    const bool onbar = R.bar > 0u;
+    const bool rule = !onbar && nd_by_rule(R);
+    rcnt = 0;
+    if (!onbar && !rule) return -1;
+    const uint32_t occ = occ24(R.m0, R.m1, R.m2);
+    auto entry = [&](int d) -> int { return p0 ? d - 1 : 24 - d; };
+    auto open = [&](int d) -> bool { return !((R.block >> entry(d)) & 1u); };
+    // first moves per die (wave-uniform): die d owns lanes [st(d), st(d) + n(d)),
+    // dice descending; the lane's die is the lowest d with st(d) <= lane
+    int st = 0, dl = 6, kst = 0;
+    uint32_t srcl = 0u;
+#pragma unroll
+    for (int d = 6; d >= 1; --d) {
+        const uint32_t sd = rule ? occ & ok_mask(R.block, d, R.player) : (open(d) ? 1u : 0u);
+        if (l >= st) {
+            dl = d;
+            srcl = sd;
+            kst = st;
+        }
+        st += __popc(sd);
+    }
+    const int nf = st;
+    if (nf > 64) return -1;
+    const bool valid = l < nf;
+    // the lane's first move: source s1 (24 = the bar), destination t1, hit h1,
+    // and the occupancy of the board after it (the child's normal-move sources)
+    int s1 = 24, t1 = 0;
+    uint32_t base2 = 0u;
+    if (valid) {
+        if (rule) {
+            s1 = select_bit_fast(srcl, l - kst);
+            t1 = p0 ? s1 + dl : s1 - dl;
+            const uint32_t last1 = nib(R.m0, R.m1, R.m2, s1) == 1u ? 1u << s1 : 0u;
+            base2 = (occ & ~last1) | (1u << t1);
+        } else {
+            t1 = entry(dl);
+            base2 = occ | (1u << t1);
+        }
+    }
+    const bool h1 = valid && ((R.blot >> t1) & 1u);
+    const uint32_t pinfo = (uint32_t)s1 | ((uint32_t)t1 << 5) | (h1 ? 1u << 10 : 0u);
+    const bool child_bar = R.bar >= 2u;   // after one entry the mover is still on the bar
+    int total = 0, q = 0;
+    for (int Ld = 1; Ld <= 5; ++Ld) {
+        for (int Hd = Ld + 1; Hd <= 6; ++Hd, ++q) {
+            const bool isH = valid && dl == Hd, isL = valid && dl == Ld;
+            const uint32_t okH = ok_mask(R.block, Hd, R.player), okL = ok_mask(R.block, Ld, R.player);
+            uint32_t m2 = 0u;
+            if (isH || isL) {
+                if (child_bar) m2 = open(isH ? Ld : Hd) ? 1u << 24 : 0u;   // bit 24: the bar entry
+                else m2 = base2 & (isH ? okL : okH);
+            }
+            const bool two1 = ballot(isH && m2 != 0u) != 0ull;
+            const bool two2 = ballot(isL && m2 != 0u) != 0ull;
+            const int nH = rule ? __popc(occ & okH) : (open(Hd) ? 1 : 0);
+            int cq = 0;
+            if (two1 || (nH != 1 && two2)) {
+                // 2-move records
+                if (rule && isL) {   // a pass-1 parent adds only its chain or reverse-chain child
+                    const int rv = p0 ? s1 - Hd : s1 + Hd;
+                    m2 &= (1u << t1) | ((rv >= 0 && rv < 24) ? 1u << rv : 0u);
+                }
+                // bar mode: the pass-0 play that a pass-1 play can repeat (see above)
+                uint32_t K0 = ND_DROP;
+                if (!rule) {
+                    const int eH = entry(Hd), eL = entry(Ld);
+                    const bool hH = (R.blot >> eH) & 1u;
+                    if (child_bar) {
+                        if (open(Hd) && open(Ld))
+                            K0 = nd_key(24u, (uint32_t)eH, hH, 24u, (uint32_t)eL, ((R.blot >> eL) & 1u) != 0u);
+                    } else if (open(Hd) && ((okL >> eH) & 1u)) {
+                        const int t2 = p0 ? eH + Ld : eH - Ld;
+                        const uint32_t b2 = R.blot & ~(hH ? 1u << eH : 0u);
+                        K0 = nd_key(24u, (uint32_t)eH, hH, (uint32_t)eH, (uint32_t)t2, ((b2 >> t2) & 1u) != 0u);
+                    }
+                }
+                const int c = __popc(m2);
+                const int incl = wave_incl_scan(c);
+                const int excl = incl - c;
+                const int T = lane63(incl);
+                const uint32_t pi = pinfo | (isL ? 1u << 11 : 0u);
+                for (int b = 0; b < T; b += 64) {
+                    const int r = b + l;
+                    const int p = flat_parent<false>(map, excl, c, b);
+                    const int j = r - __shfl(excl, p, 64);
+                    const uint32_t src2 = (uint32_t)__shfl((int)m2, p, 64);
+                    const uint32_t ppi = (uint32_t)__shfl((int)pi, p, 64);
+                    const uint32_t ps1 = ppi & 31u, pt1 = (ppi >> 5) & 31u;
+                    const bool ph1 = (ppi >> 10) & 1u;
+                    const int pp = (int)((ppi >> 11) & 1u);
+                    const int s2 = (src2 >> 24) ? 24 : select_bit_fast(src2, j);
+                    const int t2 = dest_of(R, s2, pp ? Hd : Ld);
+                    const uint32_t blot2 = R.blot & ~(ph1 ? 1u << pt1 : 0u);
+                    const bool h2 = t2 < 24 && ((blot2 >> t2) & 1u);
+                    const uint32_t key = nd_key(ps1, pt1, ph1, (uint32_t)s2, (uint32_t)t2, h2);
+                    const bool keep = rule ? nd_first(R, occ, pp, (int)ps1, (int)pt1, s2, t2, Hd, Ld)
+                                           : !(pp == 1 && key == K0);
+                    const bool sv = r < T && keep;
+                    const uint64_t bm = ballot(sv);
+                    const int ns = __popcll(bm);
+                    if (total + cq + ns > LISTCAP) return -1;
+                    if (sv) list[total + cq + mask_prefix(bm)] = key;
+                    cq += ns;
+                }
+            } else {
+                // singles: high-die singles, then low-die singles unless the high
+                // die has exactly one move (handle_non_doubles 70-81; the pass-2 skip)
+                const bool sv = isH || (isL && nH != 1);
+                const uint64_t bm = ballot(sv);
+                cq = __popcll(bm);
+                if (total + cq > LISTCAP) return -1;
+                if (sv) list[total + mask_prefix(bm)] = nd_key((uint32_t)s1, (uint32_t)t1, h1, 31u, 31u, false);
+            }
+            rcnt = l == q ? cq : rcnt;
+            total += cq;
+        }
+    }
+    wave_sync();
+    return total;
+}
+
+// OUT_PACKED_FLAT rows for n records (one global atomic per chunk of rows, as
+// begin_emit); -1 = the flat buffer is full (flagged)
+BGX_DEV int reserve_flat(const MovegenArgs& a, int n, FlatCursor& fc, int want) {
+    if (n <= fc.left) {
+        const int base = fc.base;
+        fc.base += n;
+        fc.left -= n;
+        return base;
+    }
+    if (want > a.flat_chunk) want = a.flat_chunk;
+    const int grab = n > want ? n : want;
+    int base = 0;
+    if (lane_id() == 0) base = (int)atomicAdd(a.flat_count, (unsigned)grab);
+    base = uniform(base);
+    if (base + grab > a.flat_cap) {
+        if (lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
+        fc.left = 0;
+        return -1;
+    }
+    fc.base = base + n;
+    fc.left = grab - n;
+    return base;
+}
+
 // ------------------------------------------------------------------ block-cooperative doubles
 // Small launches (no more jobs than resident waves, e.g. the 1-ply step) are
 // bound by their slowest job: a doubles roll with hundreds of results. A

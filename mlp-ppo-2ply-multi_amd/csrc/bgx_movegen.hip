@@ -116,6 +116,104 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     }
 }
 
+// Tier 1 of the 2-ply reply launch, board-major (IN_TWOPLY, OUT_PACKED_FLAT):
+// the pool kernel's workgroups, slices and LDS job counter, but an item is a
+// (candidate row, group): group 0 = the row's 15 non-doubles rolls in one
+// wave (board_nd_records, one record block for the row; roots it does not
+// cover run their 15 rolls as per-roll jobs), groups 1..6 = the doubles roll
+// (d, d) as a per-roll job (job_records). Items are interleaved over the
+// workgroups (b, b + G, ...) as the pool kernel's jobs, so the heavy doubles
+// items spread. Same records, offsets and counts per job as the pool kernel
+// (job order within a row's block is the DICE_ROLLS order); overflowing
+// per-roll jobs go to tier 2 as before.
+constexpr int REPLY_GROUPS = 7;
+__global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_reply_kernel(
+    MovegenArgs a0) {
+    MovegenArgs a = a0;
+    a.in_mode = IN_TWOPLY;
+    a.out_mode = OUT_PACKED_FLAT;
+    __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
+    __shared__ int next_job;
+    const int w = (int)threadIdx.x >> 6, l = lane_id();
+    uint32_t* sl = (uint32_t*)(smem + (size_t)w * (PSL / 8));
+    Mem M;
+    M.map = sl;
+    M.tab = (unsigned long long*)(sl + 64);
+    M.S = P_S;
+    M.F = P_F;
+    M.fa = sl + 64 + 2 * P_S;
+    M.fb = M.fa + P_F;
+    M.pa = sl + 64;
+    M.pb = M.pa + P_PF;
+    M.PF = P_PF;
+    M.force_table = a.force_table;
+    M.map[l] = 0u;
+    const int n_jobs = uniform(job_count(a));
+    const int n_items = (n_jobs + 20) / 21 * REPLY_GROUPS;
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int nk = n_items > b ? (n_items - b + G - 1) / G : 0;
+    if (threadIdx.x == 0) next_job = PW;
+    __syncthreads();
+    FlatCursor fc;
+    int k = w;
+    RawJob raw;
+    if (k < nk) raw = fetch_raw(a, (b + k * G) / REPLY_GROUPS * 21);
+    // one (row, roll) job as the pool kernel runs it
+    auto per_roll = [&](int j, const RawJob& cur) {
+        const JobIn in = decode_job(a, j, cur);
+        if (in.skip) {
+            begin_emit(a, j, 0, fc);
+        } else {
+            const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc, a.heavy_t);
+            if (r < 0 && l == 0) push_ovf(a, j);
+        }
+    };
+    while (k < nk) {   // k is wave-uniform
+        int kn = 0;
+        if (l == 0) kn = atomicAdd(&next_job, 1);
+        kn = uniform(kn);
+        const int it = b + k * G;
+        const int row = it / REPLY_GROUPS, grp = it - REPLY_GROUPS * row;
+        const RawJob cur = raw;
+        if (kn < nk) raw = fetch_raw(a, (b + kn * G) / REPLY_GROUPS * 21);
+        const int left = (nk - k + PW - 1) / PW;   // items this wave still expects
+        fc.left_hint = left;
+        const int j0 = row * 21;
+        if (grp > 0) {
+            const int j = j0 + dbl_q21(grp);
+            if (j < n_jobs) per_roll(j, cur);
+        } else {
+            const JobIn in = decode_job(a, j0 + 1, cur);   // the row's root (the dice are not used)
+            int n = -1, rc = 0;
+            if (!in.skip && !a.force_table && a.force_tier < 2 && j0 + 21 <= n_jobs)
+                n = board_nd_records<P_PF>(in.R, M.map, M.pa, rc);
+            if (n >= 0) {
+                // the row's records in one block; job q's records at its prefix
+                const int base = reserve_flat(a, n, fc, 24 * 15 * left);
+                const int pre = wave_incl_scan(rc) - rc;
+                if (l < ND_ROLLS) {
+                    const int j = j0 + nd_roll_q21(l);
+                    a.job_off[j] = base < 0 ? 0 : base + pre;
+                    a.job_cnt[j] = base < 0 ? 0 : rc;
+                }
+                if (base >= 0) {
+                    for (int i = l; i < n; i += 64) {
+                        const uint32_t e = M.pa[i];
+                        emit_one(a, 0, in.R, nd_board(in.R, e), i, base);
+                    }
+                }
+                wave_sync();   // the list is read before the next item reuses the slice
+            } else {
+                for (int q = 0; q < ND_ROLLS; ++q) {
+                    const int j = j0 + nd_roll_q21(q);
+                    if (j < n_jobs) per_roll(j, cur);
+                }
+            }
+        }
+        k = kn;
+    }
+}
+
 // Tier 1 for launches with few jobs (the 1-ply step, the first 2-ply launch):
 // 16-wave blocks, one job per wave per window. The block reserves its rows of
 // the flat output with ONE atomic (a same-address global atomic costs ~11 ns
@@ -327,7 +425,16 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         int blocks = n_cu * per_cup;
         const int need = (a.n_jobs + bgx::PW - 1) / bgx::PW;
         if (!a.n_jobs_dev && need < blocks) blocks = need;
-        if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT)
+        // BGX_REPLY_BM=0: the 2-ply replies as per-(row, roll) jobs (the A/B and
+        // cross-check arm; identical records)
+        ev = getenv("BGX_REPLY_BM");
+        const bool bm = !ev || atoi(ev) != 0;
+        if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT && bm) {
+            int rb = n_cu * per_cup;
+            const int need_r = ((a.n_jobs + 20) / 21 * bgx::REPLY_GROUPS + bgx::PW - 1) / bgx::PW;
+            if (!a.n_jobs_dev && need_r < rb) rb = need_r;
+            hipLaunchKernelGGL(bgx::movegen_reply_kernel, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);
+        } else if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT)
             hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>), dim3(blocks),
                                dim3(64 * bgx::PW), 0, stream, a);
         else
