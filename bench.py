@@ -126,12 +126,15 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
     hg = None
-    if world > 1 and args.gather == "host":
-        from bgx import hostgather
-        # anonymous memory segments (memfd), not /dev/shm files: the path does
-        # not depend on the container's /dev/shm size (bgx/hostgather.py)
-        hg = hostgather.setup(rank, world, hostgather.slot_bytes_for(lanes, args.harvest_every), dst=0,
-                              device=torch.cuda.current_device())
+    if world > 1 and args.gather in ("host", "device"):
+        from bgx import devgather, hostgather
+        # host: anonymous memory segments (memfd), not /dev/shm files, so the path
+        # does not depend on the container's /dev/shm size (bgx/hostgather.py);
+        # device: slots in rank 0's GPU memory, peer copies on the DMA engines
+        # (bgx/devgather.py). Same protocol, no collective per harvest.
+        mod = hostgather if args.gather == "host" else devgather
+        hg = mod.setup(rank, world, hostgather.slot_bytes_for(lanes, args.harvest_every), dst=0,
+                       device=torch.cuda.current_device())
     seq = [0]
 
     def run(n):
@@ -148,7 +151,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
                 eng.harvest_fetch(t, wrap=False)   # the harvest ran on the device; nobody reads it here
                 return
             h = eng.harvest_fetch(t)
-            if hg is not None:      # DMA engines into host shared memory; no collective
+            if hg is not None:      # DMA engines into host shared memory / rank 0's GPU; no collective
                 seq[0] += 1
                 if rank == 0:
                     for part in hg.collect(seq[0], copy=False):
@@ -441,9 +444,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true",
                     help="1-ply: one launch per phase and step instead of the fused persistent step kernel")
-    ap.add_argument("--gather", choices=("host", "rccl"), default="host",
+    ap.add_argument("--gather", choices=("host", "device", "rccl"), default="host",
                     help="N > 1 episode gather to rank 0: 'host' = DMA-engine copies into host shared memory "
-                         "(no kernels, no collective per harvest); 'rccl' = RCCL point-to-point over xGMI")
+                         "(no kernels, no collective per harvest); 'device' = DMA-engine peer copies into rank 0's "
+                         "GPU memory (xGMI, the GPU trainer's input); 'rccl' = RCCL point-to-point over xGMI")
     ap.add_argument("--no-balance", action="store_true",
                     help="fused 1-ply: every lane runs exactly the steps of a call (lockstep) instead of the "
                          "balanced launch (a step(n) call = n x lanes lane-steps, faster workgroups run ahead)")
@@ -565,6 +569,8 @@ def main():
                                   if args.ply == 1 and not args.no_fused else "phased launches"),
                        "parallelism": ((f"lanes sharded x{world}, episode gather to rank 0 over the DMA engines "
                                         f"into page-locked host memory (memfd segments)" if args.gather == "host"
+                                        else f"lanes sharded x{world}, episode gather over the DMA engines into "
+                                        f"rank 0's GPU memory (IPC, xGMI peer copies)" if args.gather == "device"
                                         else f"lanes sharded x{world}, RCCL episode gather to rank 0 ({BACKEND})")
                                        if world > 1 else "single GPU")},
             "desync_steps": head["desync_steps"],

@@ -295,6 +295,25 @@ int bgx_copy_async(void* dst, const void* src, uint64_t bytes, int kind, void* s
 int bgx_dma_copy_d2h(void* h_dst, const void* d_src, uint64_t bytes, int device, uint64_t* ticket);
 int bgx_dma_wait(uint64_t ticket, int timeout_ms);
 
+/* Device -> device copy on a DMA engine of the source GPU (SDMA through the HSA
+ * runtime; over xGMI when the destination is another GPU's memory, e.g. a
+ * range of the trainer rank's GPU opened with bgx_ipc_open). d_dst lies in
+ * device memory of GPU dst_device (as this process numbers the GPUs), d_src in
+ * GPU src_device's. Waited for with bgx_dma_wait. Replaces, for the device
+ * hand-off of bgx/devgather.py, the reference's pickled Queue hand-off of
+ * finished Episodes (src/main.py:115-133, multi/experience_queue.py:5-13)
+ * whose consumer moves them to the trainer's device (main.py:129-133). */
+int bgx_dma_copy_d2d(void* d_dst, int dst_device, const void* d_src, int src_device, uint64_t bytes,
+                     uint64_t* ticket);
+
+/* Inter-process access to device memory (one process per GPU): export a
+ * range (handle of its allocation + the offset of d_ptr in it), open it in
+ * another process (mapped on this process's current device, peer access
+ * enabled), close it. */
+int bgx_ipc_export(const void* d_ptr, uint8_t* handle64, uint64_t* offset);
+int bgx_ipc_open(const uint8_t* handle64, uint64_t offset, void** d_ptr);
+int bgx_ipc_close(void* d_ptr, uint64_t offset);
+
 /* The 2-ply reply expansion alone (the engine's and bgx_two_ply's reply
  * launch, two_ply.py:114-133 before the value calls): for each of n candidate
  * boards, the opponent's legal afterstates for all 21 DICE_ROLLS

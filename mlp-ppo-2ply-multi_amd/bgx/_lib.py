@@ -86,6 +86,10 @@ SIGNATURES = {
     "bgx_copy_async": (c_int, [c_void_p, c_void_p, c_u64, c_int, c_void_p]),
     "bgx_dma_copy_d2h": (c_int, [c_void_p, c_void_p, c_u64, c_int, ctypes.POINTER(c_u64)]),
     "bgx_dma_wait": (c_int, [c_u64, c_int]),
+    "bgx_dma_copy_d2d": (c_int, [c_void_p, c_int, c_void_p, c_int, c_u64, ctypes.POINTER(c_u64)]),
+    "bgx_ipc_export": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_u64)]),
+    "bgx_ipc_open": (c_int, [c_void_p, c_u64, ctypes.POINTER(c_void_p)]),
+    "bgx_ipc_close": (c_int, [c_void_p, c_u64]),
     "bgx_reply_moves": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "bgx_pack": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "bgx_unpack": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),

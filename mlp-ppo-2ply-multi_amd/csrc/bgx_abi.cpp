@@ -654,6 +654,71 @@ int bgx_dma_wait(uint64_t ticket, int timeout_ms) {
     });
 }
 
+int bgx_dma_copy_d2d(void* d_dst, int dst_device, const void* d_src, int src_device, uint64_t bytes,
+                     uint64_t* ticket) {
+    return guarded("bgx_dma_copy_d2d", [&]() -> int {
+        if (!d_dst || !d_src || !ticket) return fail(BGX_E_ARG, "bgx_dma_copy_d2d: null pointer");
+        *ticket = 0;
+        if (bytes == 0) return BGX_OK;
+        DmaDev *s = nullptr, *d = nullptr;
+        if (int rc = dma_setup(src_device, &s)) return rc;
+        if (int rc = dma_setup(dst_device, &d)) return rc;
+        // an SDMA engine of the source GPU that serves this pair (xGMI engines for
+        // a peer GPU); none listed (e.g. a copy within one GPU on some drivers):
+        // the runtime's own choice
+        uint32_t mask = 0;
+        const bool eng = hsa_amd_memory_copy_engine_status(d->gpu, s->gpu, &mask) == HSA_STATUS_SUCCESS && mask != 0;
+        hsa_signal_t sig;
+        if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS)
+            return fail(BGX_E_STATE, "bgx_dma_copy_d2d: hsa_signal_create failed");
+        const hsa_status_t st =
+            eng ? hsa_amd_memory_async_copy_on_engine(d_dst, d->gpu, d_src, s->gpu, (size_t)bytes, 0, nullptr, sig,
+                                                      (hsa_amd_sdma_engine_id_t)(mask & (~mask + 1u)), true)
+                : hsa_amd_memory_async_copy(d_dst, d->gpu, d_src, s->gpu, (size_t)bytes, 0, nullptr, sig);
+        if (st != HSA_STATUS_SUCCESS) {
+            hsa_signal_destroy(sig);
+            return fail(BGX_E_STATE, "bgx_dma_copy_d2d: async copy failed (%d)", (int)st);
+        }
+        *ticket = sig.handle;
+        return BGX_OK;
+    });
+}
+
+int bgx_ipc_export(const void* d_ptr, uint8_t* handle64, uint64_t* offset) {
+    return guarded("bgx_ipc_export", [&]() -> int {
+        if (!d_ptr || !handle64 || !offset) return fail(BGX_E_ARG, "bgx_ipc_export: null pointer");
+        static_assert(sizeof(hipIpcMemHandle_t) == 64, "64-byte IPC handles");
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_ptr));
+        hipIpcMemHandle_t h;
+        HIP_TRY(hipIpcGetMemHandle(&h, (void*)base));
+        std::memcpy(handle64, &h, 64);
+        *offset = (uint64_t)((const char*)d_ptr - (const char*)base);
+        return BGX_OK;
+    });
+}
+
+int bgx_ipc_open(const uint8_t* handle64, uint64_t offset, void** d_ptr) {
+    return guarded("bgx_ipc_open", [&]() -> int {
+        if (!handle64 || !d_ptr) return fail(BGX_E_ARG, "bgx_ipc_open: null pointer");
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handle64, 64);
+        void* base = nullptr;
+        HIP_TRY(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
+        *d_ptr = (char*)base + offset;
+        return BGX_OK;
+    });
+}
+
+int bgx_ipc_close(void* d_ptr, uint64_t offset) {
+    return guarded("bgx_ipc_close", [&]() -> int {
+        if (!d_ptr) return fail(BGX_E_ARG, "bgx_ipc_close: null pointer");
+        HIP_TRY(hipIpcCloseMemHandle((char*)d_ptr - offset));
+        return BGX_OK;
+    });
+}
+
 int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, uint32_t* d_out, int cap,
                     int32_t* d_off, int32_t* d_cnt, void* stream) {
     return guarded("bgx_reply_moves", [&]() -> int {

@@ -95,19 +95,20 @@ def test_gloo_world2_gathers_real_harvests(weights_seed0):
     assert total > 100
 
 
-def _hg_rank(rank, world, port, L, steps, out):
+def _hg_rank(rank, world, port, L, steps, out, mode="host"):
     import sys
     from conftest import PKG, golden
     sys.path.insert(0, PKG)
     import torch
     import torch.distributed as dist
-    from bgx import Engine, hostgather
+    from bgx import Engine, devgather, hostgather
     from bgx import dist as bdist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    g = hostgather.setup(rank, world, hostgather.slot_bytes_for(L, steps), dst=0, device=0)
+    mod = hostgather if mode == "host" else devgather
+    g = mod.setup(rank, world, hostgather.slot_bytes_for(L, steps), dst=0, device=0)
     w = {k: golden("weights_seed0.npz")[k] for k in ("W1", "b1", "w2", "b2")}
     base, n = bdist.lane_block(rank, L)
     e = Engine(lanes=n, lane_base=base, seed=17)
@@ -118,6 +119,9 @@ def _hg_rank(rank, world, port, L, steps, out):
         h = e.harvest()
         if rank == 0:
             parts = g.collect(seq)
+            if mode == "device":   # device tensors on rank 0's GPU
+                assert all(p is None or (p[0].is_cuda and p[1].is_cuda) for p in parts)
+                parts = devgather.as_numpy(parts)
             parts[0] = (h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32))
             got.append(parts)
         else:
@@ -137,19 +141,22 @@ def _hg_rank(rank, world, port, L, steps, out):
     dist.destroy_process_group()
 
 
-def test_host_gather_world2_real_harvests(weights_seed0):
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_host_gather_world2_real_harvests(weights_seed0, mode):
     """bench.py --gather host (the path bench.py --gpus N takes, whatever
     /dev/shm holds) with real engines: two ranks on cuda:0, rank 1's harvests
     reach rank 0 through page-locked anonymous shared memory (memfd segments
     handed over by SCM_RIGHTS) by the SDMA engines (bgx_dma_copy_d2h); merged
-    == one Engine over both lane blocks."""
+    == one Engine over both lane blocks. mode "device" (bench.py --gather
+    device, bgx/devgather.py): rank 1 copies into slots on rank 0's GPU memory,
+    opened by IPC, with bgx_dma_copy_d2d; rank 0 gets device tensors."""
     from bgx import Engine
     from bgx.records import episode_bounds
     L, steps = 128, 240
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_hg_rank, args=(r, 2, port, L, steps, q)) for r in range(2)]
+    procs = [ctx.Process(target=_hg_rank, args=(r, 2, port, L, steps, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
