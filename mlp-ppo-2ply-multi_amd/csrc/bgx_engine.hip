@@ -315,28 +315,48 @@ __global__ __launch_bounds__(256) void two_ply_reduce_kernel(const float* __rest
 // (exclusive scan of their record counts) and the harvest totals, read on the
 // device so the host needs one small copy: info = {episodes, records, error
 // flags, episodes appended (incl. any past ep_cap)}; the episode list restarts.
+// An episode whose records a lane's ring has already overwritten (harvests
+// further apart than the ring allows; flagged BGX_ERRF 8 when it happened) is
+// left out: its header's word 15 (0 on the wire) holds its output index, or
+// ~0 for a left-out one, for the gather, so the output holds only intact
+// episodes and never more records than the rings (L x R).
 __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t* __restrict__ offs,
                                                             uint32_t* __restrict__ info, uint32_t* hinfo) {
-    __shared__ int wsum[16];
+    __shared__ int wsum[16], wkeep[16];
     const unsigned n_raw = *e.ep_count;
     const int n = (int)n_raw < e.ep_cap ? (int)n_raw : e.ep_cap;
     const int t = (int)threadIdx.x, w = t >> 6;
-    int carry = 0;
+    int carry = 0, kcarry = 0;
     for (int b = 0; b < n; b += 1024) {
         const int k = b + t;
-        const int c = k < n ? (int)e.ep_list[(size_t)k * EP_WORDS + 3] : 0;
-        const int incl = wave_incl_scan(c);
-        if (lane_id() == 63) wsum[w] = incl;
+        int c = 0, keep = 0;
+        uint32_t* h = e.ep_list + (size_t)k * EP_WORDS;
+        if (k < n) {
+            const int lane = (int)h[0] - e.lane_base;
+            keep = e.rec_count[lane] - h[2] <= (uint32_t)e.R ? 1 : 0;   // wrap-safe 32-bit distance
+            c = keep ? (int)h[3] : 0;
+        }
+        const int incl = wave_incl_scan(c), kincl = wave_incl_scan(keep);
+        if (lane_id() == 63) {
+            wsum[w] = incl;
+            wkeep[w] = kincl;
+        }
         __syncthreads();
-        int before = 0, total = 0;
+        int before = 0, total = 0, kbefore = 0, ktotal = 0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const int x = wsum[q];
+            const int x = wsum[q], y = wkeep[q];
             before += q < w ? x : 0;
             total += x;
+            kbefore += q < w ? y : 0;
+            ktotal += y;
         }
-        if (k < n) offs[k] = carry + before + incl - c;
+        if (k < n) {
+            offs[k] = carry + before + incl - c;
+            h[15] = keep ? (uint32_t)(kcarry + kbefore + kincl - 1) : 0xFFFFFFFFu;
+        }
         carry += total;
+        kcarry += ktotal;
         __syncthreads();
     }
     if (t == 0) {
@@ -344,7 +364,7 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
         // the flags of the steps since the previous harvest move into this one's
         // totals (exchanged with 0 in stream order: no host reset of the word
         // while the next step may already run)
-        const uint32_t v[4] = {(uint32_t)n, (uint32_t)carry, atomicExch(e.err_flags, 0u), n_raw};
+        const uint32_t v[4] = {(uint32_t)kcarry, (uint32_t)carry, atomicExch(e.err_flags, 0u), n_raw};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             info[k] = v[k];
@@ -362,18 +382,25 @@ __global__ __launch_bounds__(1024) void harvest_scan_kernel(EngineDev e, int32_t
 // harvest, step 2: copy finished episodes' headers and records out of the
 // lane rings, one wavefront per episode (four per 256-thread block, so 4,096
 // episodes are in flight at once), 16 bytes per lane (a record is three
-// uint4); persistent grid; the episode count comes from harvest_scan_kernel
+// uint4); persistent grid over the list (info[3], clamped to ep_cap); the
+// scan's output index in header word 15 (~0: left out)
 __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t* __restrict__ hdr,
                                                      const int32_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ info, uint32_t* __restrict__ hout,
                                                      uint32_t* __restrict__ out) {
-    const int n_eps = (int)info[0];
+    const int n_list = (int)info[3] < e.ep_cap ? (int)info[3] : e.ep_cap;
     constexpr int Q = REC_WORDS / 4;
     const int wpb = (int)blockDim.x >> 6, l = lane_id();
-    for (int ep = blockIdx.x * wpb + ((int)threadIdx.x >> 6); ep < n_eps; ep += gridDim.x * wpb) {
+    for (int ep = blockIdx.x * wpb + ((int)threadIdx.x >> 6); ep < n_list; ep += gridDim.x * wpb) {
         const uint32_t* h = hdr + (size_t)ep * EP_WORDS;
+        const uint32_t oi = h[15];
+        if (oi == 0xFFFFFFFFu) continue;   // its records were overwritten (flagged)
         // the header too: the episode list is refilled by the next step
-        if (l < EP_WORDS / 4) ((uint4*)(hout + (size_t)ep * EP_WORDS))[l] = ((const uint4*)h)[l];
+        if (l < EP_WORDS / 4) {
+            uint4 v = ((const uint4*)h)[l];
+            if (l == EP_WORDS / 4 - 1) v.w = 0u;   // word 15 is 0 on the wire
+            ((uint4*)(hout + (size_t)oi * EP_WORDS))[l] = v;
+        }
         const int lane = (int)h[0] - e.lane_base;
         const uint32_t first = h[2], nrec = h[3];
         const uint4* src = (const uint4*)(e.ring + (size_t)lane * e.R * REC_WORDS);

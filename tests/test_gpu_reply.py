@@ -70,7 +70,7 @@ def test_reply_kernels_agree_on_engine_records(weights_seed0, monkeypatch):
         monkeypatch.setenv("BGX_REPLY_BM", bm)
         e = Engine(lanes=320 if k_top == 4 else 48, seed=13, ply=2, k_top=k_top)
         e.set_weights(weights_seed0, temperature=1.5, version=1)
-        out = _by_episode(*_collect(e, 40 if k_top == 4 else 16, chunk=20 if k_top == 4 else 8))
+        out = _by_episode(*_collect(e, 160 if k_top == 4 else 120, chunk=40))   # games end from ~50 steps
         e.close()
         return out
 
