@@ -1210,7 +1210,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             d.HR = hr;
             ALLOC(d.hring, (size_t)L * hr * bgx::EP_WORDS);
             ALLOC(d.hepi, L);
-            ALLOC(e->fh_ctr, 2 * bgx_engine::NHB + 1);
+            ALLOC(e->fh_ctr, 3 * bgx_engine::NHB + 1);   // reservations, done, flags, commits
         }
         if (cfg->ply == 2) {
             e->jobs_cap = cfg->k_top == 4 ? L * 4 * 21 : e->cand_cap * 21;
@@ -1233,7 +1233,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             return rc;
         }
         if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess ||
-            (e->fh_ctr && hipMemset(e->fh_ctr, 0, (2 * bgx_engine::NHB + 1) * sizeof(unsigned long long)) != hipSuccess)) {
+            (e->fh_ctr && hipMemset(e->fh_ctr, 0, (3 * bgx_engine::NHB + 1) * sizeof(unsigned long long)) != hipSuccess)) {
             bgx_engine_destroy(e);
             return fail(BGX_E_HIP, "hipMemset failed");
         }
@@ -1485,6 +1485,8 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
         f.hv_next = e->fh_ctr + (b + 1) % bgx_engine::NHB;
         f.hv_flags = e->fh_ctr + bgx_engine::NHB + 1 + b;
         f.hv_next_flags = e->fh_ctr + bgx_engine::NHB + 1 + (b + 1) % bgx_engine::NHB;
+        f.hv_commit = e->fh_ctr + 2 * bgx_engine::NHB + 1 + b;
+        f.hv_next_commit = e->fh_ctr + 2 * bgx_engine::NHB + 1 + (b + 1) % bgx_engine::NHB;
         f.hv_info = e->d_info[b];
         f.hv_hinfo = e->h_info_dev + 4 * b;
         f.done_ctr = e->fh_ctr + bgx_engine::NHB;
@@ -1578,7 +1580,9 @@ int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream) {
             // the fused launches since the last ticket harvested into slot b and
             // published its totals; with none, publish the (empty) slot here
             if (!e->fh_launched)
-                HIP_TRY(bgx_launch_harvest_close(e->fh_ctr + b, e->fh_ctr + (b + 1) % bgx_engine::NHB,
+                HIP_TRY(bgx_launch_harvest_close(e->fh_ctr + 2 * bgx_engine::NHB + 1 + b,
+                                                 e->fh_ctr + (b + 1) % bgx_engine::NHB,
+                                                 e->fh_ctr + 2 * bgx_engine::NHB + 1 + (b + 1) % bgx_engine::NHB,
                                                  e->fh_ctr + bgx_engine::NHB + 1 + b,
                                                  e->fh_ctr + bgx_engine::NHB + 1 + (b + 1) % bgx_engine::NHB,
                                                  e->ctr + C_ERR, e->d_info[b], e->h_info_dev + 4 * b, s));

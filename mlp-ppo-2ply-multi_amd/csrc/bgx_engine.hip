@@ -414,12 +414,14 @@ __global__ __launch_bounds__(256) void gather_kernel(EngineDev e, const uint32_t
 }
 
 // in-kernel harvest (fused engine) with no fused launch since the last ticket:
-// the ticket's totals are whatever its counter holds (nothing was appended);
-// its flags are the accumulator plus any flag raised since (moved, not copied)
-__global__ void harvest_close_kernel(unsigned long long* ctr, unsigned long long* next, unsigned long long* flags,
+// the ticket's totals are whatever its commit counter holds (nothing was
+// appended); its flags are the accumulator plus any flag raised since (moved,
+// not copied)
+__global__ void harvest_close_kernel(unsigned long long* commit, unsigned long long* next,
+                                     unsigned long long* next_commit, unsigned long long* flags,
                                      unsigned long long* next_flags, unsigned* err_flags, uint32_t* info,
                                      uint32_t* hinfo) {
-    const unsigned long long c = *ctr;
+    const unsigned long long c = *commit;
     const uint32_t fl = atomicExch(err_flags, 0u) | (uint32_t)*flags;
     *flags = fl;
     const uint32_t v[4] = {(uint32_t)(c >> 32), (uint32_t)c, fl, (uint32_t)(c >> 32)};
@@ -429,17 +431,18 @@ __global__ void harvest_close_kernel(unsigned long long* ctr, unsigned long long
         if (hinfo) hinfo[k] = v[k];
     }
     *next = 0ull;
+    *next_commit = 0ull;
     *next_flags = 0ull;
 }
 
 }  // namespace bgx
 
-extern "C" hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next,
-                                               unsigned long long* flags, unsigned long long* next_flags,
-                                               unsigned* err_flags, uint32_t* info, uint32_t* hinfo,
-                                               hipStream_t stream) {
-    hipLaunchKernelGGL(bgx::harvest_close_kernel, dim3(1), dim3(1), 0, stream, ctr, next, flags, next_flags, err_flags,
-                       info, hinfo);
+extern "C" hipError_t bgx_launch_harvest_close(unsigned long long* commit, unsigned long long* next,
+                                               unsigned long long* next_commit, unsigned long long* flags,
+                                               unsigned long long* next_flags, unsigned* err_flags, uint32_t* info,
+                                               uint32_t* hinfo, hipStream_t stream) {
+    hipLaunchKernelGGL(bgx::harvest_close_kernel, dim3(1), dim3(1), 0, stream, commit, next, next_commit, flags,
+                       next_flags, err_flags, info, hinfo);
     return hipGetLastError();
 }
 

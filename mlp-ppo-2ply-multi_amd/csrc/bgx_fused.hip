@@ -516,27 +516,23 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                     hs[64 + l] = (uint32_t)(ir - nr);
                 }
                 if (l == 0) {
-                    // the group's place in the ticket's output, reserved only if the
-                    // whole group fits (several launches between two tickets append
-                    // to one output); a group that does not fit keeps its episodes
-                    // in the rings for the next ticket
+                    // the group's place in the ticket's output: one fetch-add of its
+                    // totals on the reservation counter (a compare-and-swap loop here
+                    // serialised the 256 workgroups that finish together: +0.24 ms per
+                    // launch). A group whose range ends past the output's capacity
+                    // (several launches between two tickets append to one output)
+                    // copies nothing and keeps its episodes in the rings for the next
+                    // ticket; every group reserved after it starts past the capacity
+                    // too, so the groups that fit are a prefix of the reservations and
+                    // their sum (the commit counter) is the ticket's contiguous total
                     unsigned long long base = 0ull;
                     uint32_t fit = 1u;
                     if (te | tr) {
-                        unsigned long long old = __hip_atomic_load(f.hv_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        for (;;) {
-                            if ((old >> 32) + te > (unsigned long long)f.hv_ep_cap ||
-                                (old & 0xFFFFFFFFull) + tr > (unsigned long long)f.hv_rec_cap) {
-                                fit = 0u;
-                                break;
-                            }
-                            const unsigned long long prev = atomicCAS(f.hv_ctr, old, old + (((unsigned long long)te << 32) | tr));
-                            if (prev == old) {
-                                base = old;
-                                break;
-                            }
-                            old = prev;
-                        }
+                        const unsigned long long add = ((unsigned long long)te << 32) | tr;
+                        base = atomicAdd(f.hv_ctr, add);
+                        fit = (base >> 32) + te <= (unsigned long long)f.hv_ep_cap &&
+                              (base & 0xFFFFFFFFull) + tr <= (unsigned long long)f.hv_rec_cap;
+                        if (fit) atomicAdd(f.hv_commit, add);
                     }
                     hs[128] = te;
                     hs[129] = tr;
@@ -626,7 +622,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 if (f.budget > 0) __hip_atomic_store(f.budget_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (f.hv_hdr) {
-                    const unsigned long long c = __hip_atomic_load(f.hv_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long c = __hip_atomic_load(f.hv_commit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     // the launch's flags move into this ticket's accumulator (stream
                     // order: the fetch never resets the engine word behind a launch)
                     const uint32_t fl = atomicExch(e.err_flags, 0u) | (uint32_t)*f.hv_flags;
@@ -639,6 +635,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                         if (f.hv_hinfo) f.hv_hinfo[k] = v[k];   // host-mapped (vector stores)
                     }
                     __hip_atomic_store(f.hv_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(f.hv_next_commit, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 __hip_atomic_store(f.done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }

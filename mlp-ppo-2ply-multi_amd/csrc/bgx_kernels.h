@@ -54,6 +54,8 @@ struct MovegenArgs {
     int force_table;             // test hook (BGX_MG_TEST_TABLE=1): every job takes the hash-table path
                                  //   (no table-free doubles / non-doubles rules), as a cross-check
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
+    int reply_groups;            // tools hook (BGX_REPLY_GROUPS, tools/reply_micro.py): run only the
+                                 //   reply items of these groups (bit 0: non-doubles, bit d: (d, d)); 0 = all
     unsigned* err_flags;
 };
 
@@ -184,8 +186,10 @@ struct FusedArgs {
     uint32_t* hv_rec;            // [L * R][REC_WORDS]
     int hv_ep_cap;               // headers the output holds
     long long hv_rec_cap;        // records the output holds (L x R)
-    unsigned long long* hv_ctr;  // this output's running totals
+    unsigned long long* hv_ctr;  // this output's reservations (fetch-add of a group's totals)
     unsigned long long* hv_next; // the next output's (zeroed by the last workgroup)
+    unsigned long long* hv_commit;       // this output's totals: the groups that fit (published)
+    unsigned long long* hv_next_commit;  // the next output's (zeroed by the last workgroup)
     unsigned long long* hv_flags;       // this output's accumulated error flags
     unsigned long long* hv_next_flags;  // the next output's (zeroed by the last workgroup)
     uint32_t* hv_info;           // [4] device
@@ -241,9 +245,9 @@ hipError_t bgx_launch_harvest_scan(const bgx::EngineDev* e, int32_t* offsets, ui
 // in-kernel harvest bookkeeping when no fused launch ran since the last ticket:
 // publish the (empty) totals of ctr with the accumulated error flags (the
 // engine's flags moved in) and zero the next output's counter and flags
-hipError_t bgx_launch_harvest_close(unsigned long long* ctr, unsigned long long* next, unsigned long long* flags,
-                                    unsigned long long* next_flags, unsigned* err_flags, uint32_t* info,
-                                    uint32_t* hinfo, hipStream_t stream);
+hipError_t bgx_launch_harvest_close(unsigned long long* commit, unsigned long long* next, unsigned long long* next_commit,
+                                    unsigned long long* flags, unsigned long long* next_flags, unsigned* err_flags,
+                                    uint32_t* info, uint32_t* hinfo, hipStream_t stream);
 hipError_t bgx_launch_harvest_gather(const bgx::EngineDev* e, const int32_t* offsets, const uint32_t* info,
                                      uint32_t* hout, uint32_t* out, hipStream_t stream);
 }

@@ -449,17 +449,42 @@ BGX_DEV int job_count(const MovegenArgs& a) {
 // of a 2-ply launch serialises at the memory side).
 // left_hint >= 0: the jobs this wave still expects (kernels that do not
 // stride by gridDim.x set it per job; begin_emit sizes its reservation by it)
-struct FlatCursor { int base = 0, left = 0, left_hint = -1; };
+// (base2, left2): the larger remainder of an earlier chunk, kept when a request
+// did not fit it (a 2-ply row block of ~200 rows would otherwise leave up to a
+// block's worth of gap rows per chunk, which the reply MLP evaluates)
+struct FlatCursor { int base = 0, left = 0, left_hint = -1, base2 = 0, left2 = 0; };
+
+// n rows from the cursor's current or kept remainder; false: neither holds them
+BGX_DEV bool cursor_take(FlatCursor& fc, int n, int& base) {
+    if (n <= fc.left) {
+        base = fc.base;
+        fc.base += n;
+        fc.left -= n;
+        return true;
+    }
+    if (n <= fc.left2) {
+        base = fc.base2;
+        fc.base2 += n;
+        fc.left2 -= n;
+        return true;
+    }
+    return false;
+}
+// a new chunk replaces the current one; the larger of the two remainders is kept
+BGX_DEV void cursor_new_chunk(FlatCursor& fc, int base, int n, int grab) {
+    if (fc.left > fc.left2) {
+        fc.base2 = fc.base;
+        fc.left2 = fc.left;
+    }
+    fc.base = base + n;
+    fc.left = grab - n;
+}
 
 // reserve output space once the job's record count is known; returns base (-1: overflow)
 BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
     int base = 0;
     if (a.out_mode == OUT_PACKED_FLAT) {
-        if (n <= fc.left) {
-            base = fc.base;
-            fc.base += n;
-            fc.left -= n;
-        } else {
+        if (!cursor_take(fc, n, base)) {
             // chunk = min(flat_chunk, 32 rows per job this wave still has), at least n
             const int left_jobs =
                 fc.left_hint >= 0 ? fc.left_hint : (job_count(a) - j + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -470,11 +495,10 @@ BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
             base = uniform(base);
             if (base + grab > a.flat_cap) {
                 if (lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
-                fc.left = 0;
+                fc.left = fc.left2 = 0;
                 base = -1;
             } else {
-                fc.base = base + n;
-                fc.left = grab - n;
+                cursor_new_chunk(fc, base, n, grab);
             }
         }
         if (lane_id() == 0) {
@@ -1048,24 +1072,18 @@ BGX_DEV int board_nd_records(const Root& R, uint32_t* map, uint32_t* list, int& 
 // OUT_PACKED_FLAT rows for n records (one global atomic per chunk of rows, as
 // begin_emit); -1 = the flat buffer is full (flagged)
 BGX_DEV int reserve_flat(const MovegenArgs& a, int n, FlatCursor& fc, int want) {
-    if (n <= fc.left) {
-        const int base = fc.base;
-        fc.base += n;
-        fc.left -= n;
-        return base;
-    }
+    int base = 0;
+    if (cursor_take(fc, n, base)) return base;
     if (want > a.flat_chunk) want = a.flat_chunk;
     const int grab = n > want ? n : want;
-    int base = 0;
     if (lane_id() == 0) base = (int)atomicAdd(a.flat_count, (unsigned)grab);
     base = uniform(base);
     if (base + grab > a.flat_cap) {
         if (lane_id() == 0) atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
-        fc.left = 0;
+        fc.left = fc.left2 = 0;
         return -1;
     }
-    fc.base = base + n;
-    fc.left = grab - n;
+    cursor_new_chunk(fc, base, n, grab);
     return base;
 }
 

@@ -176,6 +176,10 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         const int row = it / REPLY_GROUPS, grp = it - REPLY_GROUPS * row;
         const RawJob cur = raw;
         if (kn < nk) raw = fetch_raw(a, (b + kn * G) / REPLY_GROUPS * 21);
+        if (a.reply_groups && !((a.reply_groups >> grp) & 1)) {   // tools hook: timing by group
+            k = kn;
+            continue;
+        }
         const int left = (nk - k + PW - 1) / PW;   // items this wave still expects
         fc.left_hint = left;
         const int j0 = row * 21;
@@ -406,6 +410,8 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
     const int fewm = ev ? atoi(ev) : -1;
     a.force_tier = test_tier;
     a.force_table = test_table;
+    ev = getenv("BGX_REPLY_GROUPS");
+    a.reply_groups = ev ? (int)strtol(ev, nullptr, 0) : 0;
     // doubles run table-free in tier 1 (the block-cooperative hand-off of heavy
     // doubles measured slower since then: DESIGN.md §4)
     a.heavy_t = 0x7FFFFFFF;
