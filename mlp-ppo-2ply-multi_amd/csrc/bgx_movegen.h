@@ -895,9 +895,144 @@ BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const ui
     }
 }
 
+// A doubles job by path (doubles_by_path) whose depth-4 leaves are written
+// straight to the output instead of the slice's list: levels 1-3 as
+// job_records, then the level-3 parents twice -- once to count the leaves
+// (the output rows are reserved for them), once to expand and emit them in
+// first-reach order, each leaf's board built from its path. The list then
+// holds at most level 3, so a job with hundreds of results (1-1 / 2-2 with
+// many movable checkers: the 2-ply replies' usual tier-2 jobs) fits tier 1.
+// Same records as job_records + emit_records. -1: a level-1..3 list outgrew
+// the slice (tier 2).
 template <bool G>
+BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc) {
+    const Root& R = in.R;
+    const int l = lane_id();
+    const int d = in.d0;
+    const uint32_t okd = ok_mask(R.block, d, R.player);
+    uint32_t* fa = M.pa ? M.pa : M.fa;
+    uint32_t* fb = M.pa ? M.pb : M.fb;
+    const int PFc = M.pa ? M.PF : M.F;
+    if (l == 0) st32<G>(fa, PATH_EMPTY);
+    sync<G>();
+    // a parent's filtered move list (lane-local): node, bar entry, first-reach filter
+    auto parent = [&](uint32_t path, Moves& pm, uint32_t& one) {
+        uint32_t bad, occ;
+        const Node nd = path_node(R, path, d, okd, bad, occ);
+        pm = path_moves(R, nd, occ, d, okd);
+        one = pm.n == 1 ? FLAG1 : 0u;
+        pm.src &= ~bad;
+        pm.nsrc = __popc(pm.src);
+    };
+    int n = 1, level = 0;
+    while (level < 3) {
+        int nn = 0;
+        for (int b = 0; b < n; b += 64) {
+            const int i = b + l;
+            const bool live = i < n;
+            const uint32_t path = live ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
+            Moves pm;
+            uint32_t one;
+            parent(path, pm, one);
+            const int c = live ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0;
+            const int incl = wave_incl_scan(c);
+            const int excl = incl - c;
+            const int Tc = lane63(incl);
+            if (n_out_check(nn, Tc, PFc)) return -1;
+            for (int cb = 0; cb < Tc; cb += 64) {
+                const int r = cb + l;
+                const int p = flat_parent<G>(M.map, excl, c, cb);
+                const int jj = r - __shfl(excl, p, 64);
+                const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+                const int nsrc = __shfl(pm.nsrc, p, 64);
+                const int e0 = __shfl(pm.e0, p, 64);
+                const uint32_t pp = (uint32_t)__shfl((int)path, p, 64);
+                const uint32_t tag = (uint32_t)__shfl((int)one, p, 64);
+                const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
+                const uint32_t child = (pp & ~(31u << (5 * level))) | ((uint32_t)sx << (5 * level));
+                if (r < Tc) st32<G>(fb + nn + r, child | tag | PATHF);
+            }
+            nn += Tc;
+        }
+        sync<G>();
+        if (nn == 0) break;
+        uint32_t* t = fa; fa = fb; fb = t;
+        n = nn;
+        ++level;
+    }
+    // the leaves (level 4) of the n level-3 parents: count them
+    int T4 = 0;
+    if (level == 3) {
+        for (int b = 0; b < n; b += 64) {
+            const int i = b + l;
+            const uint32_t path = i < n ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
+            Moves pm;
+            uint32_t one;
+            parent(path, pm, one);
+            T4 += lane63(wave_incl_scan(i < n ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0));
+        }
+    }
+    if (T4 == 0) {
+        // the tree ends above depth 4: the deepest level's nodes whose parent had
+        // one move (none at level 0), as job_records
+        int nfin = 0;
+        if (level > 0) {
+            for (int b = 0; b < n; b += 64) {
+                const int i = b + l;
+                const uint32_t e = i < n ? ld32<G>(fa + i) : 0u;
+                const bool rec = i < n && (e & FLAG1);
+                const uint64_t bm = ballot(rec);
+                sync<G>();
+                if (rec) st32<G>(fa + nfin + mask_prefix(bm), e);
+                nfin += __popcll(bm);
+                sync<G>();
+            }
+        }
+        const int base = begin_emit(a, j, nfin, fc);
+        if (base >= 0) emit_records<G>(a, j, in, fa, nfin, base);
+        return nfin;
+    }
+    const int base = begin_emit(a, j, T4, fc);
+    if (base < 0) return T4;   // the flat buffer is full (flagged)
+    int done = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + l;
+        const bool live = i < n;
+        const uint32_t path = live ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
+        Moves pm;
+        uint32_t one;
+        parent(path, pm, one);
+        const int c = live ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0;
+        const int incl = wave_incl_scan(c);
+        const int excl = incl - c;
+        const int Tc = lane63(incl);
+        for (int cb = 0; cb < Tc; cb += 64) {
+            const int r = cb + l;
+            const int p = flat_parent<G>(M.map, excl, c, cb);
+            const int jj = r - __shfl(excl, p, 64);
+            const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+            const int nsrc = __shfl(pm.nsrc, p, 64);
+            const int e0 = __shfl(pm.e0, p, 64);
+            const uint32_t pp = (uint32_t)__shfl((int)path, p, 64);
+            const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
+            const uint32_t leaf = (pp & ~(31u << 15)) | ((uint32_t)sx << 15);
+            if (r < Tc) emit_one(a, j, R, path_board(R, leaf, d), done + r, base);
+        }
+        done += Tc;
+    }
+    sync<G>();
+    return T4;
+}
+
+// LEAF: path doubles write their leaves directly (path_doubles_emit); the
+// large launches (pool / reply kernels) use it, the fused 1-ply kernel keeps
+// job_records (its registers are at the cap)
+template <bool G, bool LEAF = false>
 BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc,
                     int heavy_t = 0x7FFFFFFF) {
+    if constexpr (LEAF) {
+        if (in.d0 == in.d1 && doubles_by_path(in.R) && !M.force_table) return path_doubles_emit<G>(a, j, in, M, fc);
+    }
     uint32_t* fin = nullptr;
     const int nfin = job_records<G>(in, M, fin, heavy_t);
     if (nfin < 0) return nfin;

@@ -97,19 +97,21 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     FlatCursor fc;
     int k = w;
     RawJob raw;
-    if (k < nk) raw = fetch_raw(a, b + k * G);
+    // job k of this workgroup (through the list of deferred reply jobs, if any)
+    auto job_of = [&](int kk) -> int { return a.job_list ? a.job_list[b + kk * G] : b + kk * G; };
+    if (k < nk) raw = fetch_raw(a, job_of(k));
     while (k < nk) {   // k is wave-uniform
         int kn = 0;
         if (l == 0) kn = atomicAdd(&next_job, 1);
         kn = uniform(kn);
-        const int j = b + k * G;
+        const int j = uniform(job_of(k));
         const JobIn in = decode_job(a, j, raw);
-        if (kn < nk) raw = fetch_raw(a, b + kn * G);
+        if (kn < nk) raw = fetch_raw(a, job_of(kn));
         fc.left_hint = (nk - k + PW - 1) / PW;
         if (in.skip) {
             begin_emit(a, j, 0, fc);
         } else {
-            const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc, a.heavy_t);
+            const int r = a.force_tier >= 2 ? -1 : run_job<false, true>(a, j, in, M, fc, a.heavy_t);
             if (r < 0 && l == 0) push_ovf(a, j);
         }
         k = kn;
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         if (in.skip) {
             begin_emit(a, j, 0, fc);
         } else {
-            const int r = a.force_tier >= 2 ? -1 : run_job<false>(a, j, in, M, fc, a.heavy_t);
+            const int r = a.force_tier >= 2 ? -1 : run_job<false, true>(a, j, in, M, fc, a.heavy_t);
             if (r < 0 && l == 0) push_ovf(a, j);
         }
     };
@@ -207,6 +209,14 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                     }
                 }
                 wave_sync();   // the list is read before the next item reuses the slice
+            } else if (a.defer_list && !in.skip && j0 + 21 <= n_jobs) {
+                // not covered (bear-off range, or a test hook): its 15 rolls go to
+                // the balanced pool launch that follows, instead of 15 jobs in a row
+                // on this wave (the launch's tail)
+                int slot = 0;
+                if (l == 0) slot = (int)atomicAdd(a.defer_count, (unsigned)ND_ROLLS);
+                slot = uniform(slot);
+                if (l < ND_ROLLS && slot + l < a.defer_cap) a.defer_list[slot + l] = j0 + nd_roll_q21(l);
             } else {
                 for (int q = 0; q < ND_ROLLS; ++q) {
                     const int j = j0 + nd_roll_q21(q);
@@ -440,6 +450,18 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
             const int need_r = ((a.n_jobs + 20) / 21 * bgx::REPLY_GROUPS + bgx::PW - 1) / bgx::PW;
             if (!a.n_jobs_dev && need_r < rb) rb = need_r;
             hipLaunchKernelGGL(bgx::movegen_reply_kernel, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);
+            if (a.defer_list) {   // the deferred per-roll jobs, balanced over the whole grid
+                e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                bgx::MovegenArgs d = a;
+                d.n_jobs = 0;
+                d.n_jobs_dev = a.defer_count;
+                d.jobs_per_dev_unit = 1;
+                d.n_jobs_max = a.defer_cap;
+                d.job_list = a.defer_list;
+                hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>),
+                                   dim3(n_cu * per_cup), dim3(64 * bgx::PW), 0, stream, d);
+            }
         } else if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT)
             hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>), dim3(blocks),
                                dim3(64 * bgx::PW), 0, stream, a);
