@@ -16,6 +16,7 @@
 #include <exception>
 #include <new>
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -148,7 +149,6 @@ struct bgx_engine {
     int32_t* job_off = nullptr;
     int32_t* job_cnt = nullptr;
     float* job_val = nullptr;
-    int32_t* defer_list = nullptr;   // 2-ply: reply jobs deferred to the pool launch (movegen_reply_kernel)
     int jobs_cap = 0, reply_cap = 0, cand_cap = 0;
     int32_t* ovf_list = nullptr;
     int ovf_cap = 0;
@@ -205,7 +205,7 @@ struct bgx_engine {
 };
 
 namespace {
-constexpr int C_EP = 3, C_ERR = 4, C_DEFER = 5, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
+constexpr int C_EP = 3, C_ERR = 4, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
 constexpr int C_BUDGET = 12;   // [12..15]: the balanced fused launch's lane-step and finished-workgroup counters (u64)
 }
 
@@ -737,11 +737,11 @@ int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, u
         uint8_t* mover = nullptr;
         uint32_t *rows = nullptr, *ws = nullptr;
         unsigned* ctr = nullptr;
-        int32_t *ovf = nullptr, *defer = nullptr;
+        int32_t* ovf = nullptr;
         int rc = BGX_OK;
         const int ws_waves = 64, ws_slots = 16384, ovf_cap = 1 << 16;
         if (dalloc(&mover, n) || dalloc(&rows, (size_t)n * 8) || dalloc(&ctr, 8) || dalloc(&ovf, ovf_cap) ||
-            dalloc(&ws, (size_t)ws_waves * 5 * ws_slots) || dalloc(&defer, (size_t)n * 21))
+            dalloc(&ws, (size_t)ws_waves * 5 * ws_slots))
             rc = BGX_E_HIP;
         if (!rc) {
             std::vector<uint8_t> ho(n), hm(n);
@@ -771,15 +771,12 @@ int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, u
             b.ws_slots = ws_slots;
             b.ws_words_per_wave = (size_t)5 * ws_slots;
             b.err_flags = ctr + 3;
-            b.defer_list = defer;
-            b.defer_count = ctr + 5;
-            b.defer_cap = n * 21;
             if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
         }
         unsigned flags = 0;
         if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
             rc = BGX_E_HIP;
-        void* ps[] = {mover, rows, ctr, ovf, ws, defer};
+        void* ps[] = {mover, rows, ctr, ovf, ws};
         for (void* p : ps) hipFree(p);
         if (rc) return fail(rc, "bgx_reply_moves: HIP failure");
         if (flags) return fail(BGX_E_CAPACITY, "bgx_reply_moves: overflow flags 0x%x", flags);
@@ -907,13 +904,13 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
         uint8_t* mover = nullptr;
         uint32_t *rows = nullptr, *reply = nullptr, *ws = nullptr;
         unsigned* ctr = nullptr;
-        int32_t *off = nullptr, *cnt = nullptr, *ovf = nullptr, *defer = nullptr;
+        int32_t *off = nullptr, *cnt = nullptr, *ovf = nullptr;
         float *V = nullptr, *jv = nullptr;
         int rc = BGX_OK;
         const int ws_waves = 64, ws_slots = 16384, ovf_cap = 1 << 16;
         if (dalloc(&mover, n) || dalloc(&rows, (size_t)n * 8) || dalloc(&reply, (size_t)cap * 8) ||
             dalloc(&ctr, 8) || dalloc(&off, jobs) || dalloc(&cnt, jobs) || dalloc(&V, cap) || dalloc(&jv, jobs) ||
-            dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots) || dalloc(&defer, jobs)) {
+            dalloc(&ovf, ovf_cap) || dalloc(&ws, (size_t)ws_waves * 5 * ws_slots)) {
             rc = BGX_E_HIP;
         }
         std::vector<uint8_t> hm;
@@ -949,9 +946,6 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
             b.ws_slots = ws_slots;
             b.ws_words_per_wave = (size_t)5 * ws_slots;
             b.err_flags = ctr + 3;
-            b.defer_list = defer;
-            b.defer_count = ctr + 5;
-            b.defer_cap = jobs;
             if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
         }
         if (!rc) {
@@ -974,7 +968,7 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
         unsigned flags = 0;
         if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
             rc = BGX_E_HIP;
-        void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws, defer};
+        void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws};
         for (void* p : ps) hipFree(p);
         if (rc) return fail(rc, "bgx_two_ply: HIP failure");
         if (flags) return fail(BGX_E_CAPACITY, "bgx_two_ply: overflow flags 0x%x", flags);
@@ -1107,7 +1101,7 @@ int bgx_engine_destroy(bgx_engine* e) {
             hipFree(e->fprof);
         }
         void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
-                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->defer_list, e->ovf_list, e->ws, e->out_records[0],
+                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records[0],
                       e->out_records[1], e->out_records[2], e->out_headers[0], e->out_headers[1], e->out_headers[2],
                       e->d_offs[0], e->d_offs[1], e->d_offs[2], e->d_info[2], e->fh_ctr, e->d.hring, e->d.hepi,
                       e->d_info[0], e->d_info[1], e->fcand, e->fvbuf, e->ft1cnt, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
@@ -1233,7 +1227,6 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             ALLOC(e->job_off, e->jobs_cap);
             ALLOC(e->job_cnt, e->jobs_cap);
             ALLOC(e->job_val, e->jobs_cap);
-            ALLOC(e->defer_list, e->jobs_cap);   // >= 15 x the reply rows of a step
         }
     #undef ALLOC
         if (rc) {
@@ -1273,7 +1266,6 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         d.reply_count = e->ctr + C_REPLY;
         d.ovf_count = e->ctr + C_OVF;
         d.ovf_count2 = e->ctr + C_OVF2;
-        d.defer_count = e->ctr + C_DEFER;
         d.n_jobs2 = cfg->k_top == 4 ? L * 4 * 21 : 0;
         d.stats = e->stats;
         d.err_flags = e->ctr + C_ERR;
@@ -1424,9 +1416,6 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             b.job_cnt = e->job_cnt;
             mg_common(e, b);
             b.ovf_count = e->ctr + C_OVF2;
-            b.defer_list = e->defer_list;
-            b.defer_count = e->ctr + C_DEFER;
-            b.defer_cap = e->jobs_cap;
             if (timed(e, 0, s, true)) return BGX_E_HIP;
             HIP_TRY(bgx_launch_movegen(&b, s));
             if (timed(e, 0, s, false)) return BGX_E_HIP;
@@ -1612,6 +1601,25 @@ int bgx_harvest_enqueue(bgx_engine* e, int* ticket, void* stream) {
     });
 }
 
+// Wait for a harvest event: poll it for up to 2 ms (a short launch's harvest
+// lands within that; a blocking wait adds the runtime's wake-up after the
+// kernel ends), then block. BGX_SPIN_WAIT=0: block at once (A/B).
+static hipError_t wait_event(hipEvent_t ev) {
+    static const int spin = [] {
+        const char* v = getenv("BGX_SPIN_WAIT");
+        return v ? atoi(v) : 1;
+    }();
+    if (spin) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipEventQuery(ev);
+            if (q != hipErrorNotReady) return q;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) break;
+        }
+    }
+    return hipEventSynchronize(ev);
+}
+
 int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out) {
     return guarded("bgx_harvest_fetch", [&]() -> int {
         if (!e || !out) return fail(BGX_E_ARG, "bgx_harvest_fetch: null pointer");
@@ -1620,7 +1628,7 @@ int bgx_harvest_fetch(bgx_engine* e, int ticket, bgx_harvest_info* out) {
                         ticket, e->h_tickets);
         HIP_TRY(hipSetDevice(e->device));
         const int b = ticket % bgx_engine::NHB;
-        HIP_TRY(hipEventSynchronize(e->hdone[b]));
+        HIP_TRY(wait_event(e->hdone[b]));
         // the ticket's own flags: its harvest (or the last launch before it)
         // moved them out of the engine word on the device, in stream order
         const uint32_t* info = e->h_info + 4 * b;

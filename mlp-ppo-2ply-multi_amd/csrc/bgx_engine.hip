@@ -72,7 +72,6 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
         *e.reply_count = 0u;
         *e.ovf_count = 0u;
         *e.ovf_count2 = 0u;
-        *e.defer_count = 0u;
     }
     // one game lane per half-wave (8 per 256-thread block), as in the fused engine
     __shared__ float xs[8][512];

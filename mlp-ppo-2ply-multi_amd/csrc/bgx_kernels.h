@@ -54,10 +54,6 @@ struct MovegenArgs {
     int force_table;             // test hook (BGX_MG_TEST_TABLE=1): every job takes the hash-table path
                                  //   (no table-free doubles / non-doubles rules), as a cross-check
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
-    const int32_t* job_list;     // pool kernel: job k is job_list[k] (the deferred reply jobs), else k
-    int32_t* defer_list;         // reply kernel: the 15 non-doubles jobs of roots it does not cover go
-    unsigned* defer_count;       //   here (one pool launch over them follows, balanced), if non-null
-    int defer_cap;               //   (>= 15 x rows: never full)
     int reply_groups;            // tools hook (BGX_REPLY_GROUPS, tools/reply_micro.py): run only the
                                  //   reply items of these groups (bit 0: non-doubles, bit d: (d, d)); 0 = all
     unsigned* err_flags;
@@ -135,7 +131,6 @@ struct EngineDev {
     unsigned* reply_count;       // 2-ply reply rows this step (device; zeroed by the step kernel)
     unsigned* ovf_count;         // jobs sent to the fallback path this step (device)
     unsigned* ovf_count2;        // same, for the 2-ply reply launch
-    unsigned* defer_count;       // 2-ply reply jobs deferred to the pool launch this step (device)
     int n_jobs2;                 // 2-ply jobs this step when k_top = 4
     unsigned long long* stats;   // [8] env steps, decisions, episodes, value rows, movegen jobs, fallback
     unsigned* err_flags;

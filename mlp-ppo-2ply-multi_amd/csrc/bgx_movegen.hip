@@ -97,16 +97,14 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     FlatCursor fc;
     int k = w;
     RawJob raw;
-    // job k of this workgroup (through the list of deferred reply jobs, if any)
-    auto job_of = [&](int kk) -> int { return a.job_list ? a.job_list[b + kk * G] : b + kk * G; };
-    if (k < nk) raw = fetch_raw(a, job_of(k));
+    if (k < nk) raw = fetch_raw(a, b + k * G);
     while (k < nk) {   // k is wave-uniform
         int kn = 0;
         if (l == 0) kn = atomicAdd(&next_job, 1);
         kn = uniform(kn);
-        const int j = uniform(job_of(k));
+        const int j = b + k * G;
         const JobIn in = decode_job(a, j, raw);
-        if (kn < nk) raw = fetch_raw(a, job_of(kn));
+        if (kn < nk) raw = fetch_raw(a, b + kn * G);
         fc.left_hint = (nk - k + PW - 1) / PW;
         if (in.skip) {
             begin_emit(a, j, 0, fc);
@@ -129,6 +127,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
 // (job order within a row's block is the DICE_ROLLS order); overflowing
 // per-roll jobs go to tier 2 as before.
 constexpr int REPLY_GROUPS = 7;
+constexpr int REPLY_SUBQ = 1024;   // sub-queue entries per workgroup (4 KB of LDS: 2 x 68 KB per CU)
 __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_reply_kernel(
     MovegenArgs a0) {
     MovegenArgs a = a0;
@@ -154,7 +153,17 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     const int n_items = (n_jobs + 20) / 21 * REPLY_GROUPS;
     const int G = (int)gridDim.x, b = (int)blockIdx.x;
     const int nk = n_items > b ? (n_items - b + G - 1) / G : 0;
-    if (threadIdx.x == 0) next_job = PW;
+    // the workgroup's sub-queue: the 15 per-roll jobs of a root that
+    // board_nd_records does not cover are shared by its waves (entry = job + 1,
+    // 0 until the pushing wave has written it) instead of running in a row on
+    // one wave (at ~13 us per job that wave ends ~190 us after the others)
+    __shared__ int subq[REPLY_SUBQ];
+    __shared__ int sub_res, sub_head, items_done;
+    for (int i = (int)threadIdx.x; i < REPLY_SUBQ; i += 64 * PW) subq[i] = 0;
+    if (threadIdx.x == 0) {
+        next_job = PW;
+        sub_res = sub_head = items_done = 0;
+    }
     __syncthreads();
     FlatCursor fc;
     int k = w;
@@ -170,7 +179,46 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
             if (r < 0 && l == 0) push_ovf(a, j);
         }
     };
-    while (k < nk) {   // k is wave-uniform
+    auto lds_ld = [](int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    for (unsigned spin = 0;;) {
+        // 1. a queued sub-job first (short; its root's item is done)
+        int got = -1;
+        if (l == 0) {
+            int h = lds_ld(&sub_head);
+            while (h < lds_ld(&sub_res)) {
+                const int prev = atomicCAS(&sub_head, h, h + 1);
+                if (prev == h) {
+                    got = h;
+                    break;
+                }
+                h = prev;
+            }
+        }
+        got = uniform(got);
+        if (got >= 0) {
+            int v = 0;
+            for (unsigned sp = 0; (v = uniform(lds_ld(&subq[got]))) == 0; ++sp) {   // the pusher writes it next
+                if (sp >= (1u << 24)) {   // bounded
+                    if (l == 0) atomicOr(a.err_flags, BGX_ERRF_WAIT_BOUND);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (v > 0) per_roll(v - 1, fetch_raw(a, v - 1));
+            continue;
+        }
+        if (k >= nk) {
+            // no items left for this wave: done once every item is done (no more
+            // pushes) and the sub-queue is drained
+            if (lds_ld(&items_done) >= nk && lds_ld(&sub_head) >= lds_ld(&sub_res)) break;
+            if (++spin >= (1u << 24)) {
+                if (l == 0) atomicOr(a.err_flags, BGX_ERRF_WAIT_BOUND);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        // 2. this wave's next item
         int kn = 0;
         if (l == 0) kn = atomicAdd(&next_job, 1);
         kn = uniform(kn);
@@ -178,14 +226,12 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         const int row = it / REPLY_GROUPS, grp = it - REPLY_GROUPS * row;
         const RawJob cur = raw;
         if (kn < nk) raw = fetch_raw(a, (b + kn * G) / REPLY_GROUPS * 21);
-        if (a.reply_groups && !((a.reply_groups >> grp) & 1)) {   // tools hook: timing by group
-            k = kn;
-            continue;
-        }
         const int left = (nk - k + PW - 1) / PW;   // items this wave still expects
         fc.left_hint = left;
         const int j0 = row * 21;
-        if (grp > 0) {
+        if (a.reply_groups && !((a.reply_groups >> grp) & 1)) {
+            // tools hook: timing by group
+        } else if (grp > 0) {
             const int j = j0 + dbl_q21(grp);
             if (j < n_jobs) per_roll(j, cur);
         } else {
@@ -209,21 +255,36 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                     }
                 }
                 wave_sync();   // the list is read before the next item reuses the slice
-            } else if (a.defer_list && !in.skip && j0 + 21 <= n_jobs) {
-                // not covered (bear-off range, or a test hook): its 15 rolls go to
-                // the balanced pool launch that follows, instead of 15 jobs in a row
-                // on this wave (the launch's tail)
-                int slot = 0;
-                if (l == 0) slot = (int)atomicAdd(a.defer_count, (unsigned)ND_ROLLS);
-                slot = uniform(slot);
-                if (l < ND_ROLLS && slot + l < a.defer_cap) a.defer_list[slot + l] = j0 + nd_roll_q21(l);
             } else {
-                for (int q = 0; q < ND_ROLLS; ++q) {
-                    const int j = j0 + nd_roll_q21(q);
-                    if (j < n_jobs) per_roll(j, cur);
+                // not covered (bear-off range, or a test hook): its 15 rolls go to the
+                // sub-queue when it has room, else run here. (A balanced pool launch
+                // over all such jobs measured slower: its chunk reservations left
+                // 12 % more gap rows for the reply MLP, profiles/round4/reply/.)
+                int slot = -1;
+                if (l == 0 && j0 + 21 <= n_jobs) {
+                    int r = lds_ld(&sub_res);
+                    while (r + ND_ROLLS <= REPLY_SUBQ) {
+                        const int prev = atomicCAS(&sub_res, r, r + ND_ROLLS);
+                        if (prev == r) {
+                            slot = r;
+                            break;
+                        }
+                        r = prev;
+                    }
+                }
+                slot = uniform(slot);
+                if (slot >= 0) {
+                    if (l < ND_ROLLS) __hip_atomic_store(&subq[slot + l], j0 + nd_roll_q21(l) + 1, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    for (int q = 0; q < ND_ROLLS; ++q) {
+                        const int j = j0 + nd_roll_q21(q);
+                        if (j < n_jobs) per_roll(j, cur);
+                    }
                 }
             }
         }
+        if (l == 0) atomicAdd(&items_done, 1);
         k = kn;
     }
 }
@@ -450,18 +511,6 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
             const int need_r = ((a.n_jobs + 20) / 21 * bgx::REPLY_GROUPS + bgx::PW - 1) / bgx::PW;
             if (!a.n_jobs_dev && need_r < rb) rb = need_r;
             hipLaunchKernelGGL(bgx::movegen_reply_kernel, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);
-            if (a.defer_list) {   // the deferred per-roll jobs, balanced over the whole grid
-                e = hipGetLastError();
-                if (e != hipSuccess) return e;
-                bgx::MovegenArgs d = a;
-                d.n_jobs = 0;
-                d.n_jobs_dev = a.defer_count;
-                d.jobs_per_dev_unit = 1;
-                d.n_jobs_max = a.defer_cap;
-                d.job_list = a.defer_list;
-                hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>),
-                                   dim3(n_cu * per_cup), dim3(64 * bgx::PW), 0, stream, d);
-            }
         } else if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT)
             hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>), dim3(blocks),
                                dim3(64 * bgx::PW), 0, stream, a);
