@@ -895,15 +895,14 @@ BGX_DEV void emit_records(const MovegenArgs& a, int j, const JobIn& in, const ui
     }
 }
 
-// A doubles job by path (doubles_by_path) whose depth-4 leaves are written
-// straight to the output instead of the slice's list: levels 1-3 as
-// job_records, then the level-3 parents twice -- once to count the leaves
-// (the output rows are reserved for them), once to expand and emit them in
-// first-reach order, each leaf's board built from its path. The list then
-// holds at most level 3, so a job with hundreds of results (1-1 / 2-2 with
-// many movable checkers: the 2-ply replies' usual tier-2 jobs) fits tier 1.
-// Same records as job_records + emit_records. -1: a level-1..3 list outgrew
-// the slice (tier 2).
+// A doubles job by path (doubles_by_path) as job_records + emit_records, except
+// when the depth-4 list outgrows the slice: then the leaves are written
+// straight to the output from the level-3 list -- the level-3 parents once to
+// count the leaves (the output rows are reserved for them), once to expand and
+// emit them in first-reach order, each leaf's board built from its path. So a
+// job with hundreds of results (1-1 / 2-2 with many movable checkers: the 2-ply
+// replies' usual tier-2 jobs) stays in tier 1. Same records. -1: a level-1..3
+// list outgrew the slice (tier 2).
 template <bool G>
 BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc) {
     const Root& R = in.R;
@@ -925,7 +924,8 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
         pm.nsrc = __popc(pm.src);
     };
     int n = 1, level = 0;
-    while (level < 3) {
+    bool stream4 = false;   // the depth-4 list would outgrow the slice: stream the leaves
+    while (level < 4) {
         int nn = 0;
         for (int b = 0; b < n; b += 64) {
             const int i = b + l;
@@ -938,7 +938,11 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
             const int incl = wave_incl_scan(c);
             const int excl = incl - c;
             const int Tc = lane63(incl);
-            if (n_out_check(nn, Tc, PFc)) return -1;
+            if (n_out_check(nn, Tc, PFc)) {
+                if (level < 3) return -1;
+                stream4 = true;
+                break;
+            }
             for (int cb = 0; cb < Tc; cb += 64) {
                 const int r = cb + l;
                 const int p = flat_parent<G>(M.map, excl, c, cb);
@@ -955,28 +959,16 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
             nn += Tc;
         }
         sync<G>();
-        if (nn == 0) break;
+        if (stream4 || nn == 0) break;
         uint32_t* t = fa; fa = fb; fb = t;
         n = nn;
         ++level;
     }
-    // the leaves (level 4) of the n level-3 parents: count them
-    int T4 = 0;
-    if (level == 3) {
-        for (int b = 0; b < n; b += 64) {
-            const int i = b + l;
-            const uint32_t path = i < n ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
-            Moves pm;
-            uint32_t one;
-            parent(path, pm, one);
-            T4 += lane63(wave_incl_scan(i < n ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0));
-        }
-    }
-    if (T4 == 0) {
-        // the tree ends above depth 4: the deepest level's nodes whose parent had
-        // one move (none at level 0), as job_records
-        int nfin = 0;
-        if (level > 0) {
+    if (!stream4) {
+        // the deepest level; below depth 4 its nodes whose parent had one move
+        // (none at level 0), as job_records
+        int nfin = level == 4 ? n : 0;
+        if (level > 0 && level < 4) {
             for (int b = 0; b < n; b += 64) {
                 const int i = b + l;
                 const uint32_t e = i < n ? ld32<G>(fa + i) : 0u;
@@ -991,6 +983,18 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
         const int base = begin_emit(a, j, nfin, fc);
         if (base >= 0) emit_records<G>(a, j, in, fa, nfin, base);
         return nfin;
+    }
+    // stream the leaves of the n level-3 parents in fa: count them
+    int T4 = 0;
+    {
+        for (int b = 0; b < n; b += 64) {
+            const int i = b + l;
+            const uint32_t path = i < n ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
+            Moves pm;
+            uint32_t one;
+            parent(path, pm, one);
+            T4 += lane63(wave_incl_scan(i < n ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0));
+        }
     }
     const int base = begin_emit(a, j, T4, fc);
     if (base < 0) return T4;   // the flat buffer is full (flagged)
@@ -1024,9 +1028,9 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
     return T4;
 }
 
-// LEAF: path doubles write their leaves directly (path_doubles_emit); the
-// large launches (pool / reply kernels) use it, the fused 1-ply kernel keeps
-// job_records (its registers are at the cap)
+// LEAF: path doubles stream their leaves when the depth-4 list would outgrow
+// the slice (path_doubles_emit); the large launches (pool / reply kernels) use
+// it, the fused 1-ply kernel keeps job_records (its registers are at the cap)
 template <bool G, bool LEAF = false>
 BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, FlatCursor& fc,
                     int heavy_t = 0x7FFFFFFF) {
