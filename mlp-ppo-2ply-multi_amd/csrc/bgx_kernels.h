@@ -55,7 +55,9 @@ struct MovegenArgs {
                                  //   (no table-free doubles / non-doubles rules), as a cross-check
     int force_tier;              // test hook (BGX_MG_TEST_TIER): 2/3 = skip the LDS tiers below
     int reply_groups;            // tools hook (BGX_REPLY_GROUPS, tools/reply_micro.py): run only the
-                                 //   reply items of these groups (bit 0: non-doubles, bit d: (d, d)); 0 = all
+                                 //   reply items of these groups (bit 0: non-doubles, bit d: (d, d)); 0 = all;
+                                 //   0x80: leave roots board_nd_records does not cover out; 0x100: treat
+                                 //   every root as not covered
     unsigned* err_flags;
 };
 

@@ -50,6 +50,12 @@ namespace bgx {
 // = 8 waves per SIMD, the hardware maximum (amdgpu_waves_per_eu). Measured on
 // the 2-ply K=4 reply launch at 8,192 lanes (profiles/r2/ab_pool): 8 KB slices
 // / 5 waves per SIMD 0.64 ms, 4 KB / 7 waves 0.54 ms, 4 KB / 8 waves 0.475 ms.
+#ifndef BGX_REPLY_LEAF
+#define BGX_REPLY_LEAF 1   // A/B builds: 0 = path doubles never stream their leaves (job_records)
+#endif
+#ifndef BGX_REPLY_SUBQ
+#define BGX_REPLY_SUBQ 1   // A/B builds: 0 = an uncovered root's 15 jobs run on its own wave
+#endif
 #ifndef BGX_POOL_WPE
 #define BGX_POOL_WPE 8
 #endif
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         if (in.skip) {
             begin_emit(a, j, 0, fc);
         } else {
-            const int r = a.force_tier >= 2 ? -1 : run_job<false, true>(a, j, in, M, fc, a.heavy_t);
+            const int r = a.force_tier >= 2 ? -1 : run_job<false, BGX_REPLY_LEAF != 0>(a, j, in, M, fc, a.heavy_t);
             if (r < 0 && l == 0) push_ovf(a, j);
         }
         k = kn;
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         if (in.skip) {
             begin_emit(a, j, 0, fc);
         } else {
-            const int r = a.force_tier >= 2 ? -1 : run_job<false, true>(a, j, in, M, fc, a.heavy_t);
+            const int r = a.force_tier >= 2 ? -1 : run_job<false, BGX_REPLY_LEAF != 0>(a, j, in, M, fc, a.heavy_t);
             if (r < 0 && l == 0) push_ovf(a, j);
         }
     };
@@ -237,8 +243,9 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         } else {
             const JobIn in = decode_job(a, j0 + 1, cur);   // the row's root (the dice are not used)
             int n = -1, rc = 0;
-            if (!in.skip && !a.force_table && a.force_tier < 2 && j0 + 21 <= n_jobs)
+            if (!in.skip && !a.force_table && a.force_tier < 2 && j0 + 21 <= n_jobs && !(a.reply_groups & 0x100))
                 n = board_nd_records<P_PF>(in.R, M.map, M.pa, rc);
+            if (n < 0 && (a.reply_groups & 0x80)) n = -2;   // tools hook: leave uncovered roots out
             if (n >= 0) {
                 // the row's records in one block; job q's records at its prefix
                 const int base = reserve_flat(a, n, fc, 24 * 15 * left);
@@ -255,13 +262,13 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                     }
                 }
                 wave_sync();   // the list is read before the next item reuses the slice
-            } else {
+            } else if (n == -1) {
                 // not covered (bear-off range, or a test hook): its 15 rolls go to the
                 // sub-queue when it has room, else run here. (A balanced pool launch
                 // over all such jobs measured slower: its chunk reservations left
                 // 12 % more gap rows for the reply MLP, profiles/round4/reply/.)
                 int slot = -1;
-                if (l == 0 && j0 + 21 <= n_jobs) {
+                if (BGX_REPLY_SUBQ && l == 0 && j0 + 21 <= n_jobs) {
                     int r = lds_ld(&sub_res);
                     while (r + ND_ROLLS <= REPLY_SUBQ) {
                         const int prev = atomicCAS(&sub_res, r, r + ND_ROLLS);
