@@ -1208,6 +1208,196 @@ BGX_DEV int board_nd_records(const Root& R, uint32_t* map, uint32_t* list, int& 
     return total;
 }
 
+// The same records, all 15 rolls' children as ONE flat sequence (roll-major,
+// then parent lane, then move) cut into 64-child rounds, instead of one round
+// trip per roll: a roll has ~40 children, so per-roll rounds ran half empty
+// and the 15 dependent scan / parent-map / shuffle chains of a root were its
+// latency. Each lane is a parent in the 5 rolls that pair its die with
+// another; its children lists (m2, after the rule-mode pass-1 restriction) go
+// to an LDS table [lane][partner die] and its first move to pinfo[lane]; a
+// child finds its parent through the 64-word map (marks = start << 10 |
+// roll << 6 | lane, + 1; a max-scan carries the latest start) and reads the
+// two LDS words, so no shuffle is needed. Singles rolls (no 2-move play) give
+// each eligible parent one child: the single itself. aux: >= 64 * 7 + 16
+// words of LDS (the slice's second list).
+template <int LISTCAP>
+BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint32_t* aux, int& rcnt) {
+    const int l = lane_id();
+    const bool p0 = R.player == 0;
+    const bool onbar = R.bar > 0u;
+    const bool rule = !onbar && nd_by_rule(R);
+    rcnt = 0;
+    if (!onbar && !rule) return -1;
+    const uint32_t occ = occ24(R.m0, R.m1, R.m2);
+    auto entry = [&](int d) -> int { return p0 ? d - 1 : 24 - d; };
+    auto open = [&](int d) -> bool { return !((R.block >> entry(d)) & 1u); };
+    uint32_t* m2tab = aux;              // [64][6]: lane's children sources with partner die dB (bit 24: bar entry)
+    uint32_t* pinfo = aux + 64 * 6;     // [64]: s1 | t1 << 5 | h1 << 10 | die << 12
+    uint32_t* rcl = aux + 64 * 7;       // [16]: records per roll
+    // first moves per die (wave-uniform): die d owns lanes [st(d), st(d) + n(d)), dice descending
+    int st = 0, dl = 6, kst = 0;
+    uint32_t srcl = 0u, nmask = 0u;     // nmask: bits 5(d-1): n(d)
+#pragma unroll
+    for (int d = 6; d >= 1; --d) {
+        const uint32_t sd = rule ? occ & ok_mask(R.block, d, R.player) : (open(d) ? 1u : 0u);
+        if (l >= st) {
+            dl = d;
+            srcl = sd;
+            kst = st;
+        }
+        const int nd = __popc(sd);
+        nmask |= (uint32_t)nd << (5 * (d - 1));
+        st += nd;
+    }
+    const int nf = st;
+    if (nf > 64) return -1;
+    const bool valid = l < nf;
+    int s1 = 24, t1 = 0;
+    uint32_t base2 = 0u;
+    if (valid) {
+        if (rule) {
+            s1 = select_bit_fast(srcl, l - kst);
+            t1 = p0 ? s1 + dl : s1 - dl;
+            const uint32_t last1 = nib(R.m0, R.m1, R.m2, s1) == 1u ? 1u << s1 : 0u;
+            base2 = (occ & ~last1) | (1u << t1);
+        } else {
+            t1 = entry(dl);
+            base2 = occ | (1u << t1);
+        }
+    }
+    const bool h1 = valid && ((R.blot >> t1) & 1u);
+    const bool child_bar = R.bar >= 2u;
+    if (l < 16) rcl[l] = 0u;
+    // children lists per partner die: counts before (cu) and after (cr) the
+    // rule-mode pass-1 restriction, 5 bits each, packed by partner die
+    uint32_t cu_pack = 0u, cr_pack = 0u;
+    for (int dB = 1; dB <= 6; ++dB) {
+        uint32_t m2 = 0u;
+        if (valid && dB != dl) {
+            if (child_bar) m2 = open(dB) ? 1u << 24 : 0u;
+            else m2 = base2 & ok_mask(R.block, dB, R.player);
+        }
+        cu_pack |= (uint32_t)(__popc(m2 & 0xFFFFFFu) + (m2 >> 24)) << (5 * (dB - 1));
+        if (rule && dB > dl) {   // this lane is a pass-1 parent of (dB, dl): chain / reverse chain only
+            const int rv = p0 ? s1 - dB : s1 + dB;
+            m2 &= (1u << t1) | ((rv >= 0 && rv < 24) ? 1u << rv : 0u);
+        }
+        cr_pack |= (uint32_t)(__popc(m2 & 0xFFFFFFu) + (m2 >> 24)) << (5 * (dB - 1));
+        m2tab[l * 6 + dB - 1] = m2;
+    }
+    pinfo[l] = (uint32_t)s1 | ((uint32_t)t1 << 5) | (h1 ? 1u << 10 : 0u) | ((uint32_t)dl << 12);
+    // per roll: the mode (2-move records or singles) and the children counts;
+    // each lane keeps the flat start of its children in the (<= 5) rolls it is
+    // a parent of, packed 10 bits per partner die (3 + 3 dice per word)
+    uint32_t single_mask = 0u, st_lo = 0u, st_hi = 0u;
+    int total = 0, q = 0;
+    for (int Ld = 1; Ld <= 5; ++Ld) {
+        for (int Hd = Ld + 1; Hd <= 6; ++Hd, ++q) {
+            const bool isH = valid && dl == Hd, isL = valid && dl == Ld;
+            const int cuH = (int)((cu_pack >> (5 * (Ld - 1))) & 31u);   // a die-H lane's children with L
+            const int cuL = (int)((cu_pack >> (5 * (Hd - 1))) & 31u);   // a die-L lane's children with H
+            const bool two1 = ballot(isH && cuH > 0) != 0ull;
+            const bool two2 = ballot(isL && cuL > 0) != 0ull;
+            const int nH = (int)((nmask >> (5 * (Hd - 1))) & 31u);
+            const bool two = two1 || (nH != 1 && two2);
+            int c = 0;
+            if (two) {
+                c = isH ? (int)((cr_pack >> (5 * (Ld - 1))) & 31u) : (isL ? (int)((cr_pack >> (5 * (Hd - 1))) & 31u) : 0);
+            } else {
+                single_mask |= 1u << q;
+                c = (isH || (isL && nH != 1)) ? 1 : 0;
+            }
+            const int incl = wave_incl_scan(c);
+            const int start = total + incl - c;
+            if (c > 0) {   // this lane's start in roll q (partner die = the roll's other die)
+                const int pd = isH ? Ld : Hd;
+                const uint32_t v = (uint32_t)start & 1023u;
+                if (pd <= 3) st_lo |= v << (10 * (pd - 1));
+                else st_hi |= v << (10 * (pd - 4));
+            }
+            total += lane63(incl);
+        }
+    }
+    if (total > 1023) return -1;   // (10-bit starts; far above any root's children)
+    // the flat rounds
+    int n_out = 0;
+    uint32_t carry = 0u;
+    for (int b = 0; b < total; b += 64) {
+        // marks of the parents whose children start in this round
+        for (int pd = 1; pd <= 6; ++pd) {
+            if (pd == dl || !valid) continue;
+            const int H = pd > dl ? pd : dl, L = pd > dl ? dl : pd;
+            const bool sing = (single_mask >> (((L - 1) * (12 - L)) / 2 + (H - L - 1))) & 1u;
+            const int c = sing ? ((dl == H || (int)((nmask >> (5 * (H - 1))) & 31u) != 1) ? 1 : 0)
+                               : (int)((cr_pack >> (5 * (pd - 1))) & 31u);
+            const uint32_t s = pd <= 3 ? (st_lo >> (10 * (pd - 1))) & 1023u : (st_hi >> (10 * (pd - 4))) & 1023u;
+            if (c > 0 && (int)s >= b && (int)s < b + 64) {
+                const int qq = ((L - 1) * (12 - L)) / 2 + (H - L - 1);
+                map[s - b] = ((s << 10) | ((uint32_t)qq << 6) | (uint32_t)l) + 1u;
+            }
+        }
+        wave_sync();
+        uint32_t mk = map[l];
+        map[l] = 0u;
+        mk = (uint32_t)wave_incl_max((int)mk);
+        mk = mk ? mk : carry;
+        carry = (uint32_t)lane63((int)mk);
+        const int r = b + l;
+        const uint32_t code = (mk - 1u) & 1023u;
+        const int qq = (int)(code >> 6), p = (int)(code & 63u);
+        const int jj = r - (int)((mk - 1u) >> 10);
+        // the roll's dice (DICE_ROLLS order of the non-doubles): L from the group starts 0, 5, 9, 12, 14
+        const int L = 1 + (qq >= 5) + (qq >= 9) + (qq >= 12) + (qq >= 14);
+        const int H = L + 1 + qq - ((L - 1) * (12 - L)) / 2;
+        const uint32_t pi = pinfo[p];
+        const uint32_t ps1 = pi & 31u, pt1 = (pi >> 5) & 31u;
+        const bool ph1 = (pi >> 10) & 1u;
+        const int pdl = (int)(pi >> 12);
+        const int pp = pdl == L ? 1 : 0;   // pass 1: the parent moved the low die first
+        uint32_t key;
+        bool keep = true;
+        if ((single_mask >> qq) & 1u) {
+            key = nd_key(ps1, pt1, ph1, 31u, 31u, false);
+        } else {
+            const uint32_t src2 = m2tab[p * 6 + (pp ? H : L) - 1];
+            const int s2 = (src2 >> 24) ? 24 : select_bit_fast(src2, jj);
+            const int t2 = dest_of(R, s2, pp ? H : L);
+            const uint32_t blot2 = R.blot & ~(ph1 ? 1u << pt1 : 0u);
+            const bool h2 = t2 < 24 && ((blot2 >> t2) & 1u);
+            key = nd_key(ps1, pt1, ph1, (uint32_t)s2, (uint32_t)t2, h2);
+            if (rule) {
+                keep = nd_first(R, occ, pp, (int)ps1, (int)pt1, s2, t2, H, L);
+            } else if (pp == 1) {
+                // bar mode: the pass-0 play a pass-1 play can repeat (board_nd_records)
+                uint32_t K0 = ND_DROP;
+                const int eH = entry(H), eL = entry(L);
+                const bool hH = (R.blot >> eH) & 1u;
+                if (child_bar) {
+                    if (open(H) && open(L))
+                        K0 = nd_key(24u, (uint32_t)eH, hH, 24u, (uint32_t)eL, ((R.blot >> eL) & 1u) != 0u);
+                } else if (open(H) && ((ok_mask(R.block, L, R.player) >> eH) & 1u)) {
+                    const int t2c = p0 ? eH + L : eH - L;
+                    const uint32_t b2 = R.blot & ~(hH ? 1u << eH : 0u);
+                    K0 = nd_key(24u, (uint32_t)eH, hH, (uint32_t)eH, (uint32_t)t2c, ((b2 >> t2c) & 1u) != 0u);
+                }
+                keep = key != K0;
+            }
+        }
+        const bool sv = r < total && keep;
+        const uint64_t bm = ballot(sv);
+        const int ns = __popcll(bm);
+        if (n_out + ns > LISTCAP) return -1;
+        if (sv) {
+            list[n_out + mask_prefix(bm)] = key;
+            atomicAdd(&rcl[qq], 1u);
+        }
+        n_out += ns;
+    }
+    wave_sync();
+    rcnt = l < ND_ROLLS ? (int)rcl[l] : 0;
+    return n_out;
+}
+
 // OUT_PACKED_FLAT rows for n records (one global atomic per chunk of rows, as
 // begin_emit); -1 = the flat buffer is full (flagged)
 BGX_DEV int reserve_flat(const MovegenArgs& a, int n, FlatCursor& fc, int want) {

@@ -56,6 +56,9 @@ namespace bgx {
 #ifndef BGX_REPLY_SUBQ
 #define BGX_REPLY_SUBQ 1   // A/B builds: 0 = an uncovered root's 15 jobs run on its own wave
 #endif
+#ifndef BGX_BND
+#define BGX_BND 2          // A/B builds: 1 = the per-roll-round board_nd_records
+#endif
 #ifndef BGX_POOL_WPE
 #define BGX_POOL_WPE 8
 #endif
@@ -244,7 +247,8 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
             const JobIn in = decode_job(a, j0 + 1, cur);   // the row's root (the dice are not used)
             int n = -1, rc = 0;
             if (!in.skip && !a.force_table && a.force_tier < 2 && j0 + 21 <= n_jobs && !(a.reply_groups & 0x100))
-                n = board_nd_records<P_PF>(in.R, M.map, M.pa, rc);
+                n = BGX_BND == 2 ? board_nd_records2<P_PF>(in.R, M.map, M.pa, M.pb, rc)
+                                 : board_nd_records<P_PF>(in.R, M.map, M.pa, rc);
             if (n < 0 && (a.reply_groups & 0x80)) n = -2;   // tools hook: leave uncovered roots out
             if (n >= 0) {
                 // the row's records in one block; job q's records at its prefix

@@ -209,3 +209,115 @@ def main():
 
 if __name__ == "__main__":
     sys.exit(main())
+
+
+def board_nd_v2(R):
+    """The flat-round form (board_nd_records2): counts per (lane, partner die),
+    roll-major flat starts, 64-child rounds with marks + max-scan + carry.
+    Same {(L, H): keys} as board_nd, or None."""
+    onbar = R.bar > 0
+    rule = (not onbar) and R.rule()
+    if not onbar and not rule:
+        return None
+    occ = R.occ
+    opn = {d: not ((R.block >> R.entry(d)) & 1) for d in range(1, 7)}
+    lanes = []   # (die, s1, t1, h1, base2)
+    nd = {}
+    for d in range(6, 0, -1):
+        src = bits(occ & R.ok(d)) if rule else ([24] if opn[d] else [])
+        nd[d] = len(src)
+        for s1 in src:
+            if rule:
+                t1 = s1 + d if R.p == 0 else s1 - d
+                last1 = (1 << s1) if R.m[s1] == 1 else 0
+                base2 = (occ & ~last1) | (1 << t1)
+            else:
+                t1 = R.entry(d)
+                base2 = occ | (1 << t1)
+            lanes.append((d, s1, t1, bool((R.blot >> t1) & 1), base2))
+    if len(lanes) > 64:
+        return None
+    child_bar = R.bar >= 2
+    m2tab, cu, cr = {}, {}, {}
+    for li, (dl, s1, t1, h1, base2) in enumerate(lanes):
+        for dB in range(1, 7):
+            if dB == dl:
+                continue
+            m2 = ((1 << 24) if opn[dB] else 0) if child_bar else base2 & R.ok(dB)
+            cu[li, dB] = popc(m2)
+            if rule and dB > dl:
+                rv = s1 - dB if R.p == 0 else s1 + dB
+                m2 &= (1 << t1) | ((1 << rv) if 0 <= rv < 24 else 0)
+            cr[li, dB] = popc(m2)
+            m2tab[li, dB] = m2
+    rolls = [(L, H) for L in range(1, 6) for H in range(L + 1, 7)]
+    single, starts, total = {}, {}, 0
+    for q, (L, H) in enumerate(rolls):
+        two1 = any(lanes[i][0] == H and cu[i, L] > 0 for i in range(len(lanes)))
+        two2 = any(lanes[i][0] == L and cu[i, H] > 0 for i in range(len(lanes)))
+        nH = nd[H]
+        two = two1 or (nH != 1 and two2)
+        single[q] = not two
+        for i, ln in enumerate(lanes):
+            dl = ln[0]
+            if two:
+                c = cr[i, L] if dl == H else (cr[i, H] if dl == L else 0)
+            else:
+                c = 1 if (dl == H or (dl == L and nH != 1)) else 0
+            if c:
+                starts[i, q] = (total, c)
+                total += c
+    # rounds: each position gets its parent by the marks
+    parent_at = {}
+    for (i, q), (s, c) in starts.items():
+        for k in range(c):
+            parent_at[s + k] = (i, q, s)
+    out = {rl: [] for rl in rolls}
+    for r in range(total):
+        i, q, s = parent_at[r]
+        L, H = rolls[q]
+        dl, s1, t1, h1, base2 = lanes[i]
+        pp = 1 if dl == L else 0
+        if single[q]:
+            out[(L, H)].append(nd_key(s1, t1, h1, 31, 31, False))
+            continue
+        src2 = m2tab[i, H if pp else L]
+        s2 = 24 if src2 >> 24 else bits(src2)[r - s]
+        t2 = R.dest(s2, H if pp else L)
+        blot2 = R.blot & ~((1 << t1) if h1 else 0)
+        h2 = t2 < 24 and bool((blot2 >> t2) & 1)
+        key = nd_key(s1, t1, h1, s2, t2, h2)
+        if rule:
+            keep = nd_first(R, occ, pp, s1, t1, s2, t2, H, L)
+        else:
+            K0 = None
+            if pp == 1:
+                eH, eL = R.entry(H), R.entry(L)
+                hH = bool((R.blot >> eH) & 1)
+                if child_bar:
+                    if opn[H] and opn[L]:
+                        K0 = nd_key(24, eH, hH, 24, eL, bool((R.blot >> eL) & 1))
+                elif opn[H] and ((R.ok(L) >> eH) & 1):
+                    t2c = eH + L if R.p == 0 else eH - L
+                    b2 = R.blot & ~((1 << eH) if hH else 0)
+                    K0 = nd_key(24, eH, hH, eH, t2c, bool((b2 >> t2c) & 1))
+            keep = not (pp == 1 and key == K0)
+        if keep:
+            out[(L, H)].append(key)
+    return out
+
+
+def main_v2():
+    pos = _fuzz_positions(77, 24) + _random_positions(5, 3000)
+    bad = cov = 0
+    for b, p in pos:
+        R = Root(b, p)
+        a, v = board_nd(R), board_nd_v2(R)
+        if a is None:
+            assert v is None
+            continue
+        cov += 1
+        if a != v:
+            bad += 1
+    print(f"v2 vs v1: covered {cov}, differing roots {bad}")
+    return 1 if bad else 0
