@@ -29,6 +29,10 @@
 #include "bgx_mlp.h"
 #include "bgx_movegen.h"
 
+#ifndef BGX_FUSED_LEAF
+#define BGX_FUSED_LEAF 0   // A/B builds: 1 = tier-1 path doubles stream their leaves (run_job<LEAF>)
+#endif
+
 namespace bgx {
 
 // FL = game lanes per workgroup and NW = waves per workgroup: 16 lanes on 8
@@ -459,9 +463,15 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             T.job[v][l] = l < 7 ? st.w[l] : (uint32_t)st.p | ((uint32_t)st.d0 << 8) | ((uint32_t)st.d1 << 16);
                         const JobIn in =
                             make_job(st.w[0], st.w[1], st.w[2], st.w[3], st.w[4], st.w[5], st.w[6], st.p, st.d0, st.d1);
+#if BGX_FUSED_LEAF
+                        // path doubles stream their leaves past the slice's list (no tier 2)
+                        FlatCursor fcj;
+                        const int nf = f.force_tier >= 2 ? -1 : run_job<false, true>(a, g * FL + v, in, M1, fcj);
+#else
                         uint32_t* fin = nullptr;
                         const int nf = f.force_tier >= 2 ? -1 : job_records<false>(in, M1, fin, 0x7FFFFFFF);
                         if (nf >= 0) emit_records<false>(a, g * FL + v, in, fin, nf, 0);
+#endif
                         wave_sync();
                         if (l == 0) T.cnt[v] = nf;
                         if (prof) {
