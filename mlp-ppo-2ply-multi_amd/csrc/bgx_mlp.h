@@ -5,6 +5,10 @@
 #include "bgx_device.h"
 #include "bgx_kernels.h"
 
+#ifndef BGX_TILE_NOSKIP
+#define BGX_TILE_NOSKIP 0   // A/B builds: 1 = mlp_tile4 runs every k-step (straight-line, no zero-step branches)
+#endif
+
 namespace bgx {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -210,7 +214,7 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
         for (int r = 0; r < 16; ++r) acc[m][r] = 0.0f;
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
-        if (kmask & (1u << s)) {
+        if (BGX_TILE_NOSKIP || (kmask & (1u << s))) {
             const half8 b = feat_frag(bx, by, s, h, lut, fs);
 #pragma unroll
             for (int m = 0; m < 4; ++m) {

@@ -81,7 +81,8 @@ def main(out):
             sq = json.load(open(os.path.join(out, f"sq_{sq_leg}.json")))["kernels"]
             for g in ("movegen", "mlp", "fused"):
                 if g in legd:
-                    ks = [k for k in sq if group(k) == g and "movegen_pool" in k or (group(k) == g and g != "movegen")]
+                    # the 2-ply tier-1 reply kernel (board-major since round 4; the pool kernel before)
+                    ks = [k for k in sq if group(k) == g and (g != "movegen" or "movegen_reply" in k or "movegen_pool" in k)]
                     if ks:
                         k = ks[0]
                         for r in ("valu_busy", "mfma_busy", "lds_busy", "salu_busy", "wait_frac", "issue_stall_frac",

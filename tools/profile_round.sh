@@ -9,11 +9,11 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
 rm -rf $OUT; mkdir -p $OUT
-echo "[1/4] bench (default command)"
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
+echo "[1/4] bench (the driver command: --steps 20 --warmup 5)"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 tail -c 300 $OUT/bench.json
 echo "[2/4] kernel trace + stats of the bench command"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/ktrace.err || { tail $OUT/ktrace.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/ktrace.err || { tail $OUT/ktrace.err; exit 1; }
 echo "[3/4] PMC traffic passes"
 for leg in 1ply_fused 2ply_k4 2ply_kall; do
   if [ $leg = 1ply_fused ]; then
@@ -29,7 +29,7 @@ for leg in 1ply_fused 2ply_k4 2ply_kall; do
   done
 done
 echo "[4/4] SQ counter passes"
-bash tools/sq_counters.sh ${1:-prof} 2ply_k4 "movegen_pool|mlp_kernel_il" > /dev/null || exit 1
+bash tools/sq_counters.sh ${1:-prof} 2ply_k4 "movegen_reply|mlp_kernel_il" > /dev/null || exit 1
 bash tools/sq_counters.sh ${1:-prof} 1ply "fused_step" > /dev/null || exit 1
-bash tools/sq_counters.sh ${1:-prof} 2ply_kall "movegen_pool|mlp_kernel_il" > /dev/null || exit 1
+bash tools/sq_counters.sh ${1:-prof} 2ply_kall "movegen_reply|mlp_kernel_il" > /dev/null || exit 1
 python tools/pmc_summary.py $OUT > $OUT/pmc_traffic.json && cat $OUT/pmc_traffic.json | head -30
