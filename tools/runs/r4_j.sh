@@ -4,9 +4,9 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4j; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_reply.py tests/test_gpu_engine.py tests/test_gpu_scale.py -x -q --timeout 240 --timeout-method thread -k "reply or 2ply or two_ply or kall or same_seed" > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+BGX_LIB=tools/diag/libbgx_bnd2.so timeout -k 10 400 python -u -m pytest tests/test_gpu_reply.py tests/test_gpu_engine.py tests/test_gpu_scale.py -x -q --timeout 240 --timeout-method thread -k "reply or 2ply or two_ply or kall or same_seed" > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
 tail -1 $O/t.log
-for lib in mlp-ppo-2ply-multi_amd/bgx/libbgx.so tools/diag/libbgx_bnd1.so; do
+for lib in mlp-ppo-2ply-multi_amd/bgx/libbgx.so tools/diag/libbgx_bnd2.so; do
   for cfg in "bm:0x0" "cov:0x81"; do
     tag=$(basename $lib .so)_${cfg%%:*}; g=${cfg#*:}
     rm -rf $O/prof_$tag
@@ -27,7 +27,7 @@ print(sys.argv[2], "dispatches", n, {k: round(v / n / 32768, 1) for k, v in sort
 PY
 done
 A="--no-cpu-baseline --config1-steps 0 --timing-steps 20 --steps 20 --warmup 5 --two-ply-steps 50 --kall-steps 10"
-for rep in 1 2; do for lib in mlp-ppo-2ply-multi_amd/bgx/libbgx.so tools/diag/libbgx_bnd1.so; do
+for rep in 1 2; do for lib in mlp-ppo-2ply-multi_amd/bgx/libbgx.so tools/diag/libbgx_bnd2.so; do
   tag=$(basename $lib .so)_$rep
   BGX_LIB=$lib timeout -k 10 300 python bench.py $A > $O/b_$tag.json 2> $O/b_$tag.err || { tail -20 $O/b_$tag.err; exit 1; }
   python tools/ab_line.py $tag $O/b_$tag.json
