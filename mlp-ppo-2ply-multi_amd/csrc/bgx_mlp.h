@@ -6,7 +6,7 @@
 #include "bgx_kernels.h"
 
 #ifndef BGX_TILE_NOSKIP
-#define BGX_TILE_NOSKIP 0   // A/B builds: 1 = mlp_tile4 runs every k-step (straight-line, no zero-step branches)
+#define BGX_TILE_NOSKIP 1   // 1: mlp_tile4 runs every k-step (straight-line code); 0: zero k-steps skipped (A/B builds)
 #endif
 
 namespace bgx {

@@ -57,7 +57,7 @@ namespace bgx {
 #define BGX_REPLY_SUBQ 1   // A/B builds: 0 = an uncovered root's 15 jobs run on its own wave
 #endif
 #ifndef BGX_BND
-#define BGX_BND 1          // 2 = board_nd_records2 (flat rounds over all 15 rolls; A/B builds)
+#define BGX_BND 2          // 1 = the per-roll-round board_nd_records (A/B builds)
 #endif
 #ifndef BGX_POOL_WPE
 #define BGX_POOL_WPE 8
