@@ -1234,6 +1234,7 @@ BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint
     uint32_t* m2tab = aux;              // [64][6]: lane's children sources with partner die dB (bit 24: bar entry)
     uint32_t* pinfo = aux + 64 * 6;     // [64]: s1 | t1 << 5 | h1 << 10 | die << 12
     uint32_t* rcl = aux + 64 * 7;       // [16]: records per roll
+    uint32_t* k0tab = aux + 64 * 7 + 16;   // [16]: bar mode, the pass-0 play a pass-1 play of roll q repeats
     // first moves per die (wave-uniform): die d owns lanes [st(d), st(d) + n(d)), dice descending
     int st = 0, dl = 6, kst = 0;
     uint32_t srcl = 0u, nmask = 0u;     // nmask: bits 5(d-1): n(d)
@@ -1287,9 +1288,9 @@ BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint
     }
     pinfo[l] = (uint32_t)s1 | ((uint32_t)t1 << 5) | (h1 ? 1u << 10 : 0u) | ((uint32_t)dl << 12);
     // per roll: the mode (2-move records or singles) and the children counts;
-    // each lane keeps the flat start of its children in the (<= 5) rolls it is
-    // a parent of, packed 10 bits per partner die (3 + 3 dice per word)
-    uint32_t single_mask = 0u, st_lo = 0u, st_hi = 0u;
+    // each lane keeps, per partner die pd, its children's flat start in roll
+    // (pd, its die) as 1 << 14 | roll << 10 | start (16 bits; two partners per word)
+    uint32_t single_mask = 0u, mk01 = 0u, mk23 = 0u, mk45 = 0u;
     int total = 0, q = 0;
     for (int Ld = 1; Ld <= 5; ++Ld) {
         for (int Hd = Ld + 1; Hd <= 6; ++Hd, ++q) {
@@ -1311,11 +1312,27 @@ BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint
             const int start = total + incl - c;
             if (c > 0) {   // this lane's start in roll q (partner die = the roll's other die)
                 const int pd = isH ? Ld : Hd;
-                const uint32_t v = (uint32_t)start & 1023u;
-                if (pd <= 3) st_lo |= v << (10 * (pd - 1));
-                else st_hi |= v << (10 * (pd - 4));
+                const uint32_t v = (1u << 14 | (uint32_t)q << 10 | ((uint32_t)start & 1023u)) << (16 * ((pd - 1) & 1));
+                mk01 |= pd <= 2 ? v : 0u;
+                mk23 |= pd == 3 || pd == 4 ? v : 0u;
+                mk45 |= pd >= 5 ? v : 0u;
             }
             total += lane63(incl);
+            if (!rule && two && l == 0) {
+                // bar mode: the pass-0 play that a pass-1 play of this roll can repeat
+                uint32_t K0 = ND_DROP;
+                const int eH = entry(Hd), eL = entry(Ld);
+                const bool hH = (R.blot >> eH) & 1u;
+                if (child_bar) {
+                    if (open(Hd) && open(Ld))
+                        K0 = nd_key(24u, (uint32_t)eH, hH, 24u, (uint32_t)eL, ((R.blot >> eL) & 1u) != 0u);
+                } else if (open(Hd) && ((ok_mask(R.block, Ld, R.player) >> eH) & 1u)) {
+                    const int t2c = p0 ? eH + Ld : eH - Ld;
+                    const uint32_t b2 = R.blot & ~(hH ? 1u << eH : 0u);
+                    K0 = nd_key(24u, (uint32_t)eH, hH, (uint32_t)eH, (uint32_t)t2c, ((b2 >> t2c) & 1u) != 0u);
+                }
+                k0tab[q] = K0;
+            }
         }
     }
     if (total > 1023) return -1;   // (10-bit starts; far above any root's children)
@@ -1324,17 +1341,13 @@ BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint
     uint32_t carry = 0u;
     for (int b = 0; b < total; b += 64) {
         // marks of the parents whose children start in this round
-        for (int pd = 1; pd <= 6; ++pd) {
-            if (pd == dl || !valid) continue;
-            const int H = pd > dl ? pd : dl, L = pd > dl ? dl : pd;
-            const bool sing = (single_mask >> (((L - 1) * (12 - L)) / 2 + (H - L - 1))) & 1u;
-            const int c = sing ? ((dl == H || (int)((nmask >> (5 * (H - 1))) & 31u) != 1) ? 1 : 0)
-                               : (int)((cr_pack >> (5 * (pd - 1))) & 31u);
-            const uint32_t s = pd <= 3 ? (st_lo >> (10 * (pd - 1))) & 1023u : (st_hi >> (10 * (pd - 4))) & 1023u;
-            if (c > 0 && (int)s >= b && (int)s < b + 64) {
-                const int qq = ((L - 1) * (12 - L)) / 2 + (H - L - 1);
-                map[s - b] = ((s << 10) | ((uint32_t)qq << 6) | (uint32_t)l) + 1u;
-            }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t w = k < 2 ? mk01 : (k < 4 ? mk23 : mk45);
+            const uint32_t e = (w >> (16 * (k & 1))) & 0xFFFFu;
+            const uint32_t s = e & 1023u;
+            if ((e >> 14) && (int)s >= b && (int)s < b + 64)
+                map[s - b] = ((s << 10) | (((e >> 10) & 15u) << 6) | (uint32_t)l) + 1u;
         }
         wave_sync();
         uint32_t mk = map[l];
@@ -1368,19 +1381,7 @@ BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint
             if (rule) {
                 keep = nd_first(R, occ, pp, (int)ps1, (int)pt1, s2, t2, H, L);
             } else if (pp == 1) {
-                // bar mode: the pass-0 play a pass-1 play can repeat (board_nd_records)
-                uint32_t K0 = ND_DROP;
-                const int eH = entry(H), eL = entry(L);
-                const bool hH = (R.blot >> eH) & 1u;
-                if (child_bar) {
-                    if (open(H) && open(L))
-                        K0 = nd_key(24u, (uint32_t)eH, hH, 24u, (uint32_t)eL, ((R.blot >> eL) & 1u) != 0u);
-                } else if (open(H) && ((ok_mask(R.block, L, R.player) >> eH) & 1u)) {
-                    const int t2c = p0 ? eH + L : eH - L;
-                    const uint32_t b2 = R.blot & ~(hH ? 1u << eH : 0u);
-                    K0 = nd_key(24u, (uint32_t)eH, hH, (uint32_t)eH, (uint32_t)t2c, ((b2 >> t2c) & 1u) != 0u);
-                }
-                keep = key != K0;
+                keep = key != k0tab[qq];   // bar mode (board_nd_records)
             }
         }
         const bool sv = r < total && keep;
