@@ -183,40 +183,52 @@ BGX_DEV bool doubles_by_path(const Root& R) {
     const uint32_t home = R.player == 0 ? nibsum(R.m2 >> 8) : nibsum(R.m0 & 0xFFFFFFu);
     return 15u - R.off - home >= 5u;   // outside home (points and bar)
 }
-// node after the path's steps (abs sources, in order), its occupancy mask
-// (kept up to date per step: the source empties when it held one checker, the
-// destination fills) and the sources the path rules out: movable at an earlier
-// step and below that step's source
-BGX_DEV Node path_node(const Root& R, uint32_t path, int d, uint32_t okd, uint32_t& bad, uint32_t& occ) {
-    Node n = root_node(R);
+// The state after a path's steps (abs sources, in order) that the moves and
+// the first-reach filter need -- the mover's occupancy (kept up to date per
+// step: the source empties when it held one checker, the destination fills),
+// its bar count (returned) and the sources the path rules out (movable at an
+// earlier step and below that step's source) -- without building the board:
+// a source's count before a step is its root count plus the earlier steps
+// that landed on it minus those that left it. (path_board builds the board of
+// a record.)
+BGX_DEV uint32_t path_state(const Root& R, uint32_t path, int d, uint32_t okd, uint32_t& bad, uint32_t& occ) {
     bad = 0u;
     occ = occ24(R.m0, R.m1, R.m2);
+    uint32_t bar = R.bar;
+    int src[4], dst[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t f = (path >> (5 * i)) & 31u;
+        src[i] = -1;
+        dst[i] = -1;
         if (f != 31u) {
-            int dst;
+            int t;
             if (f < 24u) {
                 bad |= occ & okd & ((1u << f) - 1u);
-                if (nib(n.m0, n.m1, n.m2, (int)f) == 1u) occ &= ~(1u << f);
-                dst = R.player == 0 ? (int)f + d : (int)f - d;
+                int c = (int)nib(R.m0, R.m1, R.m2, (int)f);
+#pragma unroll
+                for (int j = 0; j < i; ++j) c += (dst[j] == (int)f ? 1 : 0) - (src[j] == (int)f ? 1 : 0);
+                if (c == 1) occ &= ~(1u << f);
+                t = R.player == 0 ? (int)f + d : (int)f - d;
             } else {
-                dst = R.player == 0 ? d - 1 : 24 - d;
+                bar -= 1u;
+                t = R.player == 0 ? d - 1 : 24 - d;
             }
-            n = apply_move(R, n, (int)f, d);
-            if (dst >= 0 && dst <= 23) occ |= 1u << dst;
+            src[i] = (int)f;
+            dst[i] = t;
+            if (t >= 0 && t <= 23) occ |= 1u << t;
         }
     }
-    return n;
+    return bar;
 }
 // a node's move list in a path-mode job (no node of its tree can be in
 // bear-off: doubles_by_path): the bar entry while on the bar, else every
 // occupied point whose destination is open (get_moves_bar / get_moves_normal,
 // get_moves_one_die.py:40-130) -- node_moves without the bear-off analysis
-BGX_DEV Moves path_moves(const Root& R, const Node& n, uint32_t occ, int d, uint32_t okd) {
+BGX_DEV Moves path_moves(const Root& R, uint32_t bar, uint32_t occ, int d, uint32_t okd) {
     Moves mv;
     mv.src = 0; mv.nsrc = 0; mv.e0 = -1; mv.e1 = -1; mv.n = 0;
-    if ((n.x & 15u) > 0u) {
+    if (bar > 0u) {
         const int entry = R.player == 0 ? d - 1 : 24 - d;
         if (!((R.block >> entry) & 1u)) { mv.e0 = 24; mv.n = 1; }
         return mv;
@@ -767,8 +779,8 @@ BGX_DEV int job_records(const JobIn& in, const Mem& M, uint32_t*& fin_out, int h
                     const bool live = i < n;
                     const uint32_t path = live ? ld32<G>(fa + i) & KEYMASK : PATH_EMPTY;
                     uint32_t bad, occ;
-                    const Node nd = path_node(R, path, d, okd, bad, occ);
-                    Moves pm = path_moves(R, nd, occ, d, okd);
+                    const uint32_t nbar = path_state(R, path, d, okd, bad, occ);
+                    Moves pm = path_moves(R, nbar, occ, d, okd);
                     const uint32_t one = pm.n == 1 ? FLAG1 : 0u;
                     pm.src &= ~bad;                      // e0 is the bar entry (or none) here
                     pm.nsrc = __popc(pm.src);
@@ -917,8 +929,8 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
     // a parent's filtered move list (lane-local): node, bar entry, first-reach filter
     auto parent = [&](uint32_t path, Moves& pm, uint32_t& one) {
         uint32_t bad, occ;
-        const Node nd = path_node(R, path, d, okd, bad, occ);
-        pm = path_moves(R, nd, occ, d, okd);
+        const uint32_t nbar = path_state(R, path, d, okd, bad, occ);
+        pm = path_moves(R, nbar, occ, d, okd);
         one = pm.n == 1 ? FLAG1 : 0u;
         pm.src &= ~bad;
         pm.nsrc = __popc(pm.src);
@@ -1503,8 +1515,8 @@ BGX_DEV int coop_doubles_path(const JobIn& in, L& C, uint32_t*& fin) {
                 const int i = hh * NTH + t;
                 const uint32_t path = i < n ? fa[i] & KEYMASK : PATH_EMPTY;
                 uint32_t bad, occ;
-                const Node nd = path_node(R, path, d, okd, bad, occ);
-                const Moves pm = path_moves(R, nd, occ, d, okd);
+                const uint32_t nbar = path_state(R, path, d, okd, bad, occ);
+                const Moves pm = path_moves(R, nbar, occ, d, okd);
                 const uint32_t ok = pm.src & ~bad;
                 const int ns = __popc(ok);
                 c[hh] = i < n ? ns + (pm.e0 >= 0 ? 1 : 0) : 0;
