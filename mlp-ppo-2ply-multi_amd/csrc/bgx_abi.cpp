@@ -1411,7 +1411,13 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             b.out_packed = e->reply_rows;
             b.flat_count = e->ctr + C_REPLY;
             b.flat_cap = e->reply_cap;
-            b.flat_chunk = 512;
+            // rows a wave reserves per global atomic (its unused tail is a gap row
+            // block the reply MLP evaluates); BGX_FLAT_CHUNK: A/B
+            static const int chunk = [] {
+                const char* v = getenv("BGX_FLAT_CHUNK");
+                return v && atoi(v) >= 64 ? atoi(v) : 512;
+            }();
+            b.flat_chunk = chunk;
             b.job_off = e->job_off;
             b.job_cnt = e->job_cnt;
             mg_common(e, b);
