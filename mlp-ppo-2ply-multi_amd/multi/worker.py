@@ -71,6 +71,7 @@ class Worker:
         self.max_pending = _env_int("BGX_MAX_PENDING", 2000)
         self.engines = []
         self.engine = None   # the first GPU's engine
+        self._staging = []   # per engine: page-locked host buffer for DMA-engine harvest copies
         self._pending = []   # the engines' harvest tickets of the launch in flight
 
     def _ensure_engine(self):
@@ -131,10 +132,18 @@ class Worker:
         """Advance all lanes one launch; return the previous launch's finished
         episodes as compact host arrays (headers uint32 [n, 16], records
         uint32 [m, 12]) for the bulk queue path (each episode's records
-        contiguous, in header order, GPU by GPU)."""
+        contiguous, in header order, GPU by GPU). With one GPU they are views
+        into the DMA staging buffer, valid until the next call."""
         hs = self._step_all(steps)
-        hdr = [h.headers.cpu().numpy().view(np.uint32) for h in hs]
-        rec = [h.records.cpu().numpy().view(np.uint32) for h in hs]
+        # device -> host on the DMA engines (bgx/hostcopy.py): a torch copy here
+        # is a blit kernel that would wait for the launch just queued, idling the
+        # GPU for the host's work every cycle
+        if not self._staging:
+            from bgx.hostcopy import Staging
+            self._staging = [Staging(e.device.index) for e in self.engines]
+        parts = [st.copy(h) for st, h in zip(self._staging, hs)]
+        hdr = [p[0] for p in parts]
+        rec = [p[1] for p in parts]
         if not hs:
             return np.zeros((0, 16), np.uint32), np.zeros((0, 12), np.uint32)
         if len(hs) == 1:
