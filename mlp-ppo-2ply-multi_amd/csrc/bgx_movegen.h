@@ -1040,6 +1040,170 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
     return T4;
 }
 
+// The six doubles rolls (d, d) of one root in one wave (two_ply.py:114-133),
+// for a path-mode root (doubles_by_path: no node of any of its six trees can
+// bear off). The trees expand level by level TOGETHER: a level's parents of
+// all dice form one flat sequence (die-major; each list entry carries its die
+// above the path), so the shallow levels -- one root and ~8 parents per die --
+// fill the 64 lanes instead of running six nearly empty rounds, and the root
+// is decoded once. A die whose next level is empty is finished from the
+// current list (its nodes whose parent had one move, as job_records); the
+// depth-4 leaves are counted per die, reserved and written straight to the
+// output (as path_doubles_emit). Same records, offsets and counts per job as
+// six per-roll jobs. cntd: 8 words of LDS. Returns the dice (bit d - 1) left to
+// per-roll jobs: all six when the root is not in path mode, the unfinished
+// ones when a level outgrows the slice's list.
+constexpr uint32_t DIE_SHIFT = 20;   // list entry: path | die << 20 | PATHF | FLAG1
+// index in the 21 DICE_ROLLS of the q-th non-doubles roll (the doubles sit at 0, 6, 11, 15, 18, 20)
+BGX_DEV int nd_roll_q21(int q) { return q + 1 + (q >= 5) + (q >= 9) + (q >= 12) + (q >= 14); }
+BGX_DEV int dbl_q21(int d) { return (d - 1) * 7 - ((d - 1) * d) / 2; }   // (d, d), d = 1..6
+
+template <bool G>
+BGX_DEV uint32_t board_dbl_emit(const MovegenArgs& a, int j0, const JobIn& in, const Mem& M, FlatCursor& fc,
+                                uint32_t* cntd) {
+    const Root& R = in.R;
+    const int l = lane_id();
+    if (!doubles_by_path(R) || M.force_table) return 0x3Fu;
+    uint32_t* fa = M.pa;
+    uint32_t* fb = M.pb;
+    const int PFc = M.PF;
+    const uint32_t ENTRY = KEYMASK | (7u << DIE_SHIFT);
+    if (l < 6) st32<G>(fa + l, PATH_EMPTY | ((uint32_t)(l + 1) << DIE_SHIFT));
+    // lane d (1..6): die d's first entry and entry count in the current list
+    int dfirst = l >= 1 && l <= 6 ? l - 1 : 0, dcount = l >= 1 && l <= 6 ? 1 : 0;
+    uint32_t done = 0u;   // dice finished (bit d - 1)
+    int n = 6;
+    sync<G>();
+    for (int level = 0;; ++level) {
+        const bool leaves = level == 3;   // this level's children are the records
+        if (l < 8) st32<G>(cntd + l, 0u);
+        sync<G>();
+        // one parent per lane: its die, filtered move list and child count
+        auto parent = [&](int i, uint32_t& e, int& d, Moves& pm, uint32_t& one) -> int {
+            const bool live = i < n;
+            e = live ? ld32<G>(fa + i) & ENTRY : (PATH_EMPTY | (1u << DIE_SHIFT));
+            d = (int)((e >> DIE_SHIFT) & 7u);
+            const uint32_t okd = ok_mask(R.block, d, R.player);
+            uint32_t bad, occ;
+            const uint32_t nbar = path_state(R, e & KEYMASK, d, okd, bad, occ);
+            pm = path_moves(R, nbar, occ, d, okd);
+            one = pm.n == 1 ? FLAG1 : 0u;
+            pm.src &= ~bad;
+            pm.nsrc = __popc(pm.src);
+            return live ? pm.nsrc + (pm.e0 >= 0 ? 1 : 0) : 0;
+        };
+        int nn = 0;
+        bool ovf = false;
+        for (int b = 0; b < n; b += 64) {
+            uint32_t e, one;
+            int d;
+            Moves pm;
+            const int c = parent(b + l, e, d, pm, one);
+            if (c > 0) atomicAdd(cntd + d, (uint32_t)c);
+            const int incl = wave_incl_scan(c);
+            const int excl = incl - c;
+            const int Tc = lane63(incl);
+            if (!leaves) {
+                if (n_out_check(nn, Tc, PFc)) {
+                    ovf = true;
+                    break;
+                }
+                for (int cb = 0; cb < Tc; cb += 64) {
+                    const int r = cb + l;
+                    const int p = flat_parent<G>(M.map, excl, c, cb);
+                    const int jj = r - __shfl(excl, p, 64);
+                    const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+                    const int nsrc = __shfl(pm.nsrc, p, 64);
+                    const int e0 = __shfl(pm.e0, p, 64);
+                    const uint32_t pp = (uint32_t)__shfl((int)e, p, 64);
+                    const uint32_t tag = (uint32_t)__shfl((int)one, p, 64);
+                    const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
+                    const uint32_t child = (pp & ~(31u << (5 * level))) | ((uint32_t)sx << (5 * level));
+                    if (r < Tc) st32<G>(fb + nn + r, child | tag | PATHF);
+                }
+            }
+            nn += Tc;
+        }
+        sync<G>();
+        if (ovf) return ~done & 0x3Fu;
+        const int cd = l >= 1 && l <= 6 ? (int)ld32<G>(cntd + l) : 0;   // lane d: die d's children
+        // dice whose tree ends here: their records are this level's nodes whose
+        // parent had one move (none at level 0)
+        uint32_t fin = (uint32_t)(ballot(l >= 1 && l <= 6 && cd == 0) >> 1) & ~done & 0x3Fu;
+        while (fin) {
+            const int d = __ffs(fin);
+            fin &= fin - 1u;
+            const int f0 = __builtin_amdgcn_readlane(dfirst, d), fcnt = __builtin_amdgcn_readlane(dcount, d);
+            const int j = j0 + dbl_q21(d);
+            int nrec = 0;
+            if (level > 0)
+                for (int b = 0; b < fcnt; b += 64) {
+                    const bool rec = b + l < fcnt && (ld32<G>(fa + f0 + b + l) & FLAG1);
+                    nrec += __popcll(ballot(rec));
+                }
+            const int base = begin_emit(a, j, nrec, fc);
+            if (base >= 0 && nrec > 0) {
+                int k0 = 0;
+                for (int b = 0; b < fcnt; b += 64) {
+                    const uint32_t e = b + l < fcnt ? ld32<G>(fa + f0 + b + l) : 0u;
+                    const bool rec = b + l < fcnt && (e & FLAG1);
+                    const uint64_t bm = ballot(rec);
+                    if (rec) emit_one(a, j, R, path_board(R, e & KEYMASK, d), k0 + mask_prefix(bm), base);
+                    k0 += __popcll(bm);
+                }
+            }
+            done |= 1u << (d - 1);
+        }
+        if (done == 0x3Fu) return 0u;
+        // lane d: die d's first child in the next level (children are die-major)
+        const int cincl = wave_incl_scan(cd);
+        if (!leaves) {
+            uint32_t* t = fa; fa = fb; fb = t;
+            n = nn;
+            dfirst = cincl - cd;
+            dcount = cd;
+            continue;
+        }
+        // the leaves: every remaining die's rows, then the level-3 parents again,
+        // each leaf written at its die's base + its index within the die
+        int dbase = 0;
+        for (uint32_t rem = ~done & 0x3Fu; rem; rem &= rem - 1u) {
+            const int d = __ffs(rem);
+            const int base = begin_emit(a, j0 + dbl_q21(d), __builtin_amdgcn_readlane(cd, d), fc);
+            dbase = l == d ? base : dbase;
+        }
+        const int cfirst = cincl - cd;   // lane d: die d's first leaf in the flat order
+        int done_r = 0;
+        for (int b = 0; b < n; b += 64) {
+            uint32_t e, one;
+            int d;
+            Moves pm;
+            const int c = parent(b + l, e, d, pm, one);
+            const int incl = wave_incl_scan(c);
+            const int excl = incl - c;
+            const int Tc = lane63(incl);
+            for (int cb = 0; cb < Tc; cb += 64) {
+                const int r = cb + l;
+                const int p = flat_parent<G>(M.map, excl, c, cb);
+                const int jj = r - __shfl(excl, p, 64);
+                const uint32_t src = (uint32_t)__shfl((int)pm.src, p, 64);
+                const int nsrc = __shfl(pm.nsrc, p, 64);
+                const int e0 = __shfl(pm.e0, p, 64);
+                const uint32_t pp = (uint32_t)__shfl((int)e, p, 64);
+                const int pd = (int)((pp >> DIE_SHIFT) & 7u);
+                const int base = __shfl(dbase, pd, 64), first = __shfl(cfirst, pd, 64);
+                const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
+                const uint32_t leaf = (pp & KEYMASK & ~(31u << 15)) | ((uint32_t)sx << 15);
+                if (r < Tc && base >= 0)
+                    emit_one(a, j0 + dbl_q21(pd), R, path_board(R, leaf, pd), done_r + r - first, base);
+            }
+            done_r += Tc;
+        }
+        sync<G>();
+        return 0u;
+    }
+}
+
 // LEAF: path doubles stream their leaves when the depth-4 list would outgrow
 // the slice (path_doubles_emit); the large launches (pool / reply kernels) use
 // it, the fused 1-ply kernel keeps job_records (its registers are at the cap)
@@ -1091,9 +1255,6 @@ BGX_DEV int run_job(const MovegenArgs& a, int j, const JobIn& in, const Mem& M, 
 // `rcnt` = the record count of the q-th non-doubles roll. Returns the record
 // count, or -1 (not applicable, more than 64 first moves, or the list is full).
 constexpr int ND_ROLLS = 15;
-// index in the 21 DICE_ROLLS of the q-th non-doubles roll (the doubles sit at 0, 6, 11, 15, 18, 20)
-BGX_DEV int nd_roll_q21(int q) { return q + 1 + (q >= 5) + (q >= 9) + (q >= 12) + (q >= 14); }
-BGX_DEV int dbl_q21(int d) { return (d - 1) * 7 - ((d - 1) * d) / 2; }   // (d, d), d = 1..6
 
 template <int LISTCAP>
 BGX_DEV int board_nd_records(const Root& R, uint32_t* map, uint32_t* list, int& rcnt) {

@@ -135,7 +135,10 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
 // items spread. Same records, offsets and counts per job as the pool kernel
 // (job order within a row's block is the DICE_ROLLS order); overflowing
 // per-roll jobs go to tier 2 as before.
-constexpr int REPLY_GROUPS = 7;
+#ifndef BGX_DBL_BM
+#define BGX_DBL_BM 0   // 1: a row's six doubles rolls in one item (board_dbl_emit); 0: one item per roll
+#endif
+constexpr int REPLY_GROUPS = BGX_DBL_BM ? 2 : 7;
 constexpr int REPLY_SUBQ = 1024;   // sub-queue entries per workgroup (4 KB of LDS: 2 x 68 KB per CU)
 __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_reply_kernel(
     MovegenArgs a0) {
@@ -168,6 +171,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     // one wave (at ~13 us per job that wave ends ~190 us after the others)
     __shared__ int subq[REPLY_SUBQ];
     __shared__ int sub_res, sub_head, items_done;
+    __shared__ uint32_t dcnt[PW][8];   // board_dbl_emit's per-die child counts, per wave
     for (int i = (int)threadIdx.x; i < REPLY_SUBQ; i += 64 * PW) subq[i] = 0;
     if (threadIdx.x == 0) {
         next_job = PW;
@@ -189,6 +193,31 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         }
     };
     auto lds_ld = [](int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    // cnt per-roll jobs (job_of(q), q < cnt <= 15) onto the workgroup's sub-queue
+    // when it has room (and every job index is in range), else run here
+    auto share = [&](int cnt, auto job_of, bool in_range, const RawJob& cur) {
+        int slot = -1;
+        if (BGX_REPLY_SUBQ && l == 0 && in_range) {
+            int r = lds_ld(&sub_res);
+            while (r + cnt <= REPLY_SUBQ) {
+                const int prev = atomicCAS(&sub_res, r, r + cnt);
+                if (prev == r) {
+                    slot = r;
+                    break;
+                }
+                r = prev;
+            }
+        }
+        slot = uniform(slot);
+        if (slot >= 0) {
+            if (l < cnt) __hip_atomic_store(&subq[slot + l], job_of(l) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            for (int q = 0; q < cnt; ++q) {
+                const int j = job_of(q);
+                if (j < n_jobs) per_roll(j, cur);
+            }
+        }
+    };
     for (unsigned spin = 0;;) {
         // 1. a queued sub-job first (short; its root's item is done)
         int got = -1;
@@ -240,9 +269,22 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         const int j0 = row * 21;
         if (a.reply_groups && !((a.reply_groups >> grp) & 1)) {
             // tools hook: timing by group
-        } else if (grp > 0) {
+        } else if (grp > 0 && !BGX_DBL_BM) {
             const int j = j0 + dbl_q21(grp);
             if (j < n_jobs) per_roll(j, cur);
+        } else if (grp > 0) {
+            // the six doubles rolls together (path-mode roots); the rest as per-roll
+            // jobs shared on the sub-queue
+            const JobIn in = decode_job(a, j0, cur);   // the row's root (the dice are not used)
+            uint32_t rest = 0x3Fu;
+            if (in.skip && j0 + 21 <= n_jobs) {
+                for (int d = 1; d <= 6; ++d) begin_emit(a, j0 + dbl_q21(d), 0, fc);
+                rest = 0u;
+            } else if (!in.skip && a.force_tier < 2 && j0 + 21 <= n_jobs) {
+                rest = board_dbl_emit<false>(a, j0, in, M, fc, dcnt[w]);
+            }
+            if (rest) share(__popc(rest), [&](int q) { return j0 + dbl_q21(select_bit((uint32_t)rest, q) + 1); },
+                            j0 + 21 <= n_jobs, cur);
         } else {
             const JobIn in = decode_job(a, j0 + 1, cur);   // the row's root (the dice are not used)
             int n = -1, rc = 0;
@@ -271,28 +313,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                 // sub-queue when it has room, else run here. (A balanced pool launch
                 // over all such jobs measured slower: its chunk reservations left
                 // 12 % more gap rows for the reply MLP, profiles/round4/reply/.)
-                int slot = -1;
-                if (BGX_REPLY_SUBQ && l == 0 && j0 + 21 <= n_jobs) {
-                    int r = lds_ld(&sub_res);
-                    while (r + ND_ROLLS <= REPLY_SUBQ) {
-                        const int prev = atomicCAS(&sub_res, r, r + ND_ROLLS);
-                        if (prev == r) {
-                            slot = r;
-                            break;
-                        }
-                        r = prev;
-                    }
-                }
-                slot = uniform(slot);
-                if (slot >= 0) {
-                    if (l < ND_ROLLS) __hip_atomic_store(&subq[slot + l], j0 + nd_roll_q21(l) + 1, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {
-                    for (int q = 0; q < ND_ROLLS; ++q) {
-                        const int j = j0 + nd_roll_q21(q);
-                        if (j < n_jobs) per_roll(j, cur);
-                    }
-                }
+                share(ND_ROLLS, [&](int q) { return j0 + nd_roll_q21(q); }, j0 + 21 <= n_jobs, cur);
             }
         }
         if (l == 0) atomicAdd(&items_done, 1);
