@@ -1054,6 +1054,9 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
 // per-roll jobs: all six when the root is not in path mode, the unfinished
 // ones when a level outgrows the slice's list.
 constexpr uint32_t DIE_SHIFT = 20;   // list entry: path | die << 20 | PATHF | FLAG1
+#ifndef BGX_DBL_GUARD
+#define BGX_DBL_GUARD 0   // development builds: index checks that flag (err bits 0x100..) instead of writing
+#endif
 // index in the 21 DICE_ROLLS of the q-th non-doubles roll (the doubles sit at 0, 6, 11, 15, 18, 20)
 BGX_DEV int nd_roll_q21(int q) { return q + 1 + (q >= 5) + (q >= 9) + (q >= 12) + (q >= 14); }
 BGX_DEV int dbl_q21(int d) { return (d - 1) * 7 - ((d - 1) * d) / 2; }   // (d, d), d = 1..6
@@ -1133,7 +1136,11 @@ BGX_DEV uint32_t board_dbl_emit(const MovegenArgs& a, int j0, const JobIn& in, c
         while (fin) {
             const int d = __ffs(fin);
             fin &= fin - 1u;
-            const int f0 = __builtin_amdgcn_readlane(dfirst, d), fcnt = __builtin_amdgcn_readlane(dcount, d);
+            int f0 = __builtin_amdgcn_readlane(dfirst, d), fcnt = __builtin_amdgcn_readlane(dcount, d);
+            if (BGX_DBL_GUARD && (f0 < 0 || fcnt < 0 || f0 + fcnt > n)) {
+                if (l == 0) atomicOr(a.err_flags, 0x100u);
+                f0 = fcnt = 0;
+            }
             const int j = j0 + dbl_q21(d);
             int nrec = 0;
             if (level > 0)
@@ -1148,7 +1155,13 @@ BGX_DEV uint32_t board_dbl_emit(const MovegenArgs& a, int j0, const JobIn& in, c
                     const uint32_t e = b + l < fcnt ? ld32<G>(fa + f0 + b + l) : 0u;
                     const bool rec = b + l < fcnt && (e & FLAG1);
                     const uint64_t bm = ballot(rec);
-                    if (rec) emit_one(a, j, R, path_board(R, e & KEYMASK, d), k0 + mask_prefix(bm), base);
+                    const int kk = k0 + mask_prefix(bm);
+                    bool okw = true;
+                    if (BGX_DBL_GUARD && rec && (kk >= nrec || base + kk >= a.flat_cap)) {
+                        atomicOr(a.err_flags, 0x200u);
+                        okw = false;
+                    }
+                    if (rec && okw) emit_one(a, j, R, path_board(R, e & KEYMASK, d), kk, base);
                     k0 += __popcll(bm);
                 }
             }
@@ -1192,9 +1205,18 @@ BGX_DEV uint32_t board_dbl_emit(const MovegenArgs& a, int j0, const JobIn& in, c
                 const uint32_t pp = (uint32_t)__shfl((int)e, p, 64);
                 const int pd = (int)((pp >> DIE_SHIFT) & 7u);
                 const int base = __shfl(dbase, pd, 64), first = __shfl(cfirst, pd, 64);
+                bool okw = true;
+                if (BGX_DBL_GUARD) {
+                    const int cnt = __shfl(cd, pd, 64), idx = done_r + r - first;
+                    const bool badd = pd < 1 || pd > 6 || ((done >> (pd - 1)) & 1u);
+                    if (r < Tc && (badd || idx < 0 || idx >= cnt || (base >= 0 && base + idx >= a.flat_cap))) {
+                        atomicOr(a.err_flags, badd ? 0x400u : 0x800u);
+                        okw = false;
+                    }
+                }
                 const int sx = jj < nsrc ? select_bit_fast(src, jj) : e0;
                 const uint32_t leaf = (pp & KEYMASK & ~(31u << 15)) | ((uint32_t)sx << 15);
-                if (r < Tc && base >= 0)
+                if (r < Tc && base >= 0 && okw)
                     emit_one(a, j0 + dbl_q21(pd), R, path_board(R, leaf, pd), done_r + r - first, base);
             }
             done_r += Tc;

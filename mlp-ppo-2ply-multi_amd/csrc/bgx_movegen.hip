@@ -171,7 +171,9 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     // one wave (at ~13 us per job that wave ends ~190 us after the others)
     __shared__ int subq[REPLY_SUBQ];
     __shared__ int sub_res, sub_head, items_done;
+#if BGX_DBL_BM
     __shared__ uint32_t dcnt[PW][8];   // board_dbl_emit's per-die child counts, per wave
+#endif
     for (int i = (int)threadIdx.x; i < REPLY_SUBQ; i += 64 * PW) subq[i] = 0;
     if (threadIdx.x == 0) {
         next_job = PW;
@@ -193,6 +195,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         }
     };
     auto lds_ld = [](int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+#if BGX_DBL_BM
     // cnt per-roll jobs (job_of(q), q < cnt <= 15) onto the workgroup's sub-queue
     // when it has room (and every job index is in range), else run here
     auto share = [&](int cnt, auto job_of, bool in_range, const RawJob& cur) {
@@ -218,6 +221,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
             }
         }
     };
+#endif
     for (unsigned spin = 0;;) {
         // 1. a queued sub-job first (short; its root's item is done)
         int got = -1;
@@ -272,6 +276,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         } else if (grp > 0 && !BGX_DBL_BM) {
             const int j = j0 + dbl_q21(grp);
             if (j < n_jobs) per_roll(j, cur);
+#if BGX_DBL_BM
         } else if (grp > 0) {
             // the six doubles rolls together (path-mode roots); the rest as per-roll
             // jobs shared on the sub-queue
@@ -285,6 +290,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
             }
             if (rest) share(__popc(rest), [&](int q) { return j0 + dbl_q21(select_bit((uint32_t)rest, q) + 1); },
                             j0 + 21 <= n_jobs, cur);
+#endif
         } else {
             const JobIn in = decode_job(a, j0 + 1, cur);   // the row's root (the dice are not used)
             int n = -1, rc = 0;
@@ -313,7 +319,28 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                 // sub-queue when it has room, else run here. (A balanced pool launch
                 // over all such jobs measured slower: its chunk reservations left
                 // 12 % more gap rows for the reply MLP, profiles/round4/reply/.)
-                share(ND_ROLLS, [&](int q) { return j0 + nd_roll_q21(q); }, j0 + 21 <= n_jobs, cur);
+                int slot = -1;
+                if (BGX_REPLY_SUBQ && l == 0 && j0 + 21 <= n_jobs) {
+                    int r = lds_ld(&sub_res);
+                    while (r + ND_ROLLS <= REPLY_SUBQ) {
+                        const int prev = atomicCAS(&sub_res, r, r + ND_ROLLS);
+                        if (prev == r) {
+                            slot = r;
+                            break;
+                        }
+                        r = prev;
+                    }
+                }
+                slot = uniform(slot);
+                if (slot >= 0) {
+                    if (l < ND_ROLLS) __hip_atomic_store(&subq[slot + l], j0 + nd_roll_q21(l) + 1, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    for (int q = 0; q < ND_ROLLS; ++q) {
+                        const int j = j0 + nd_roll_q21(q);
+                        if (j < n_jobs) per_roll(j, cur);
+                    }
+                }
             }
         }
         if (l == 0) atomicAdd(&items_done, 1);

@@ -1,0 +1,156 @@
+// tests/cpuwave/hip/hip_runtime.h -- test infrastructure, NOT product code.
+// A host emulation of one 64-lane wavefront for the movegen device headers
+// (csrc/bgx_movegen.h, bgx_device.h): each lane is a host thread, every
+// cross-lane operation (ballot, shuffles, readlane, DPP) is an exchange
+// through a shared buffer between two barriers, so code whose cross-lane
+// operations are reached by every lane runs as on the GPU, and host tools
+// (AddressSanitizer) see its LDS slices and output buffers. Only what those
+// headers use is provided.
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <barrier>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <type_traits>
+
+#define __device__
+#define __host__
+#define __global__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+typedef int hipError_t;
+typedef void* hipStream_t;
+
+struct uint4 { uint32_t x, y, z, w; };
+inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return {x, y, z, w}; }
+struct emu_dim3 { unsigned x, y, z; };
+
+namespace emu {
+inline thread_local int lane = 0;
+inline std::barrier<>* bar = nullptr;
+inline uint64_t xbuf[64];
+#ifdef EMU_TRACE
+}  // namespace emu
+#include <execinfo.h>
+namespace emu {
+inline void* where[64][8];
+inline int nwhere[64];
+inline unsigned long long nsync[64];
+inline void sync() {
+    nwhere[lane] = backtrace(where[lane], 8);
+    ++nsync[lane];
+    bar->arrive_and_wait();
+}
+#else
+inline void sync() { bar->arrive_and_wait(); }
+#endif
+// every lane's v (as 64-bit words)
+template <class T> inline void gather(T v, T* out) {
+    static_assert(sizeof(T) <= 8, "scalar exchange");
+    uint64_t u = 0;
+    std::memcpy(&u, &v, sizeof(T));
+    xbuf[lane] = u;
+    sync();
+    for (int i = 0; i < 64; ++i) std::memcpy(&out[i], &xbuf[i], sizeof(T));
+    sync();
+}
+template <class T> inline T lane_value(T v, int k) {
+    T all[64];
+    gather(v, all);
+    return all[k & 63];
+}
+}  // namespace emu
+
+#define threadIdx (emu_dim3{(unsigned)emu::lane, 0u, 0u})
+#define blockIdx (emu_dim3{0u, 0u, 0u})
+#define gridDim (emu_dim3{1u, 1u, 1u})
+#define blockDim (emu_dim3{64u, 1u, 1u})
+
+inline unsigned __lane_id() { return (unsigned)emu::lane; }
+inline uint64_t __ballot(bool p) {
+    bool all[64];
+    emu::gather(p, all);
+    uint64_t m = 0;
+    for (int i = 0; i < 64; ++i) m |= (uint64_t)all[i] << i;
+    return m;
+}
+template <class T> inline T __shfl(T v, int src, int width = 64) { (void)width; return emu::lane_value(v, src); }
+template <class T> inline T __shfl_xor(T v, int m, int width = 64) { (void)width; return emu::lane_value(v, emu::lane ^ m); }
+inline int __popc(uint32_t v) { return __builtin_popcount(v); }
+inline int __popcll(uint64_t v) { return __builtin_popcountll(v); }
+inline int __ffs(uint32_t v) { return __builtin_ffs((int)v); }
+inline int __ffsll(uint64_t v) { return __builtin_ffsll((long long)v); }
+inline int __clz(uint32_t v) { return v ? __builtin_clz(v) : 32; }
+inline int __clzll(long long v) { return v ? __builtin_clzll((unsigned long long)v) : 64; }
+inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+inline float __int_as_float(int v) { float f; std::memcpy(&f, &v, 4); return f; }
+inline int __float_as_int(float f) { int v; std::memcpy(&v, &f, 4); return v; }
+inline unsigned long long wall_clock64() { return 0ull; }
+inline void __syncthreads() { emu::sync(); }
+
+#define __builtin_amdgcn_readlane(v, k) emu::lane_value((int)(v), (int)(k))
+#define __builtin_amdgcn_readfirstlane(v) emu::lane_value((int)(v), 0)
+#define __builtin_amdgcn_s_memtime() 0ull
+#define __builtin_amdgcn_s_sleep(n) std::this_thread::yield()
+#define __builtin_amdgcn_fence(...) std::atomic_thread_fence(std::memory_order_seq_cst)
+#define __builtin_amdgcn_wave_barrier() emu::sync()
+inline uint32_t emu_mbcnt_lo(uint32_t m, uint32_t acc) {
+    const int l = emu::lane;
+    return acc + (uint32_t)__builtin_popcount(l >= 32 ? m : (m & ((1u << l) - 1u)));
+}
+inline uint32_t emu_mbcnt_hi(uint32_t m, uint32_t acc) {
+    const int l = emu::lane;
+    return acc + (uint32_t)(l < 32 ? 0 : __builtin_popcount(m & (uint32_t)((1ull << (l - 32)) - 1ull)));
+}
+#define __builtin_amdgcn_mbcnt_lo(m, acc) emu_mbcnt_lo((m), (acc))
+#define __builtin_amdgcn_mbcnt_hi(m, acc) emu_mbcnt_hi((m), (acc))
+// DPP for the controls the headers use: row_shr:1..15 (0x111..0x11F),
+// row_bcast:15 (0x142), row_bcast:31 (0x143)
+inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mask, bool bound_ctrl) {
+    (void)bank_mask;
+    int all[64];
+    emu::gather(src, all);
+    const int l = emu::lane, row = l >> 4;
+    if (!((row_mask >> row) & 1)) return old;
+    int from = -1;
+    if (ctrl >= 0x111 && ctrl <= 0x11F) {
+        const int n = ctrl - 0x110;
+        if ((l & 15) >= n) from = l - n;
+    } else if (ctrl == 0x142) {
+        if (row >= 1) from = 16 * row - 1;
+    } else if (ctrl == 0x143) {
+        if (row >= 2) from = 31;
+    } else {
+        std::abort();
+    }
+    if (from < 0) return bound_ctrl ? 0 : old;
+    return all[from];
+}
+#define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) emu_update_dpp((old), (src), (ctrl), (rm), (bm), (bc))
+
+#define __HIP_MEMORY_SCOPE_WAVEFRONT 1
+#define __HIP_MEMORY_SCOPE_WORKGROUP 2
+#define __HIP_MEMORY_SCOPE_AGENT 3
+#define __HIP_MEMORY_SCOPE_SYSTEM 4
+#define __hip_atomic_load(p, order, scope) __atomic_load_n((p), __ATOMIC_SEQ_CST)
+#define __hip_atomic_store(p, v, order, scope) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
+template <class T> inline T emu_fetch_min(T* p, std::type_identity_t<T> v) {
+    T cur = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+    while (v < cur && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+    }
+    return cur;
+}
+#define __hip_atomic_fetch_min(p, v, order, scope) emu_fetch_min((p), (v))
+#define __hip_atomic_fetch_add(p, v, order, scope) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
+#define __hip_atomic_compare_exchange_strong(p, cmp, v, o1, o2, scope) \
+    __atomic_compare_exchange_n((p), (cmp), (v), false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)
+template <class T> inline T atomicAdd(T* p, std::type_identity_t<T> v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+template <class T> inline T atomicOr(T* p, std::type_identity_t<T> v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
+template <class T> inline T atomicMin(T* p, std::type_identity_t<T> v) { return emu_fetch_min(p, v); }
+template <class T> inline T atomicCAS(T* p, std::type_identity_t<T> cmp, std::type_identity_t<T> v) {
+    __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
+    return cmp;
+}
