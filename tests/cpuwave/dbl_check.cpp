@@ -129,6 +129,7 @@ int main(int argc, char** argv) {
 
     auto lane_main = [&](int lane) {
         emu::lane = lane;
+        emu::tid = lane;
         for (int i = 0; i < n_cases; ++i) {
             // the jobs in every lane's registers (make_job reads lanes: all lanes run it)
             JobIn in[7];

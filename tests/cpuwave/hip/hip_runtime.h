@@ -15,6 +15,8 @@
 #include <cstring>
 #include <thread>
 #include <type_traits>
+#include <memory>
+#include <vector>
 
 #define __device__
 #define __host__
@@ -29,32 +31,48 @@ inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return
 struct emu_dim3 { unsigned x, y, z; };
 
 namespace emu {
-inline thread_local int lane = 0;
-inline std::barrier<>* bar = nullptr;
-inline uint64_t xbuf[64];
+// one emulated wavefront: its exchange buffer and its 64-lane barrier
+struct Wave {
+    std::barrier<>* bar = nullptr;
+    uint64_t xbuf[64];
+};
+inline thread_local int lane = 0;          // lane in the wave
+inline thread_local int tid = 0;           // thread in the workgroup
+inline thread_local unsigned block = 0;    // workgroup index
+inline thread_local Wave* cur = nullptr;   // this thread's wave (null: the single wave below)
+inline unsigned grid = 1, block_threads = 64;
+inline std::barrier<>* bar = nullptr;      // single-wave programs (dbl_check): its barrier
+inline Wave single;
+inline std::barrier<>* block_bar = nullptr;
+inline Wave& W() {
+    if (cur) return *cur;
+    single.bar = bar;
+    return single;
+}
 #ifdef EMU_TRACE
 }  // namespace emu
 #include <execinfo.h>
 namespace emu {
-inline void* where[64][8];
-inline int nwhere[64];
-inline unsigned long long nsync[64];
+inline void* where[1024][8];
+inline int nwhere[1024];
+inline unsigned long long nsync[1024];
 inline void sync() {
-    nwhere[lane] = backtrace(where[lane], 8);
-    ++nsync[lane];
-    bar->arrive_and_wait();
+    nwhere[tid] = backtrace(where[tid], 8);
+    ++nsync[tid];
+    W().bar->arrive_and_wait();
 }
 #else
-inline void sync() { bar->arrive_and_wait(); }
+inline void sync() { W().bar->arrive_and_wait(); }
 #endif
 // every lane's v (as 64-bit words)
 template <class T> inline void gather(T v, T* out) {
     static_assert(sizeof(T) <= 8, "scalar exchange");
+    Wave& w = W();
     uint64_t u = 0;
     std::memcpy(&u, &v, sizeof(T));
-    xbuf[lane] = u;
+    w.xbuf[lane] = u;
     sync();
-    for (int i = 0; i < 64; ++i) std::memcpy(&out[i], &xbuf[i], sizeof(T));
+    for (int i = 0; i < 64; ++i) std::memcpy(&out[i], &w.xbuf[i], sizeof(T));
     sync();
 }
 template <class T> inline T lane_value(T v, int k) {
@@ -64,10 +82,10 @@ template <class T> inline T lane_value(T v, int k) {
 }
 }  // namespace emu
 
-#define threadIdx (emu_dim3{(unsigned)emu::lane, 0u, 0u})
-#define blockIdx (emu_dim3{0u, 0u, 0u})
-#define gridDim (emu_dim3{1u, 1u, 1u})
-#define blockDim (emu_dim3{64u, 1u, 1u})
+#define threadIdx (emu_dim3{(unsigned)(emu::cur ? emu::tid : emu::lane), 0u, 0u})
+#define blockIdx (emu_dim3{emu::block, 0u, 0u})
+#define gridDim (emu_dim3{emu::grid, 1u, 1u})
+#define blockDim (emu_dim3{emu::block_threads, 1u, 1u})
 
 inline unsigned __lane_id() { return (unsigned)emu::lane; }
 inline uint64_t __ballot(bool p) {
@@ -89,7 +107,10 @@ inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)
 inline float __int_as_float(int v) { float f; std::memcpy(&f, &v, 4); return f; }
 inline int __float_as_int(float f) { int v; std::memcpy(&v, &f, 4); return v; }
 inline unsigned long long wall_clock64() { return 0ull; }
-inline void __syncthreads() { emu::sync(); }
+inline void __syncthreads() {
+    if (emu::block_bar) emu::block_bar->arrive_and_wait();
+    else emu::sync();
+}
 
 #define __builtin_amdgcn_readlane(v, k) emu::lane_value((int)(v), (int)(k))
 #define __builtin_amdgcn_readfirstlane(v) emu::lane_value((int)(v), 0)
@@ -154,3 +175,57 @@ template <class T> inline T atomicCAS(T* p, std::type_identity_t<T> cmp, std::ty
     __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
     return cmp;
 }
+
+// ---- workgroup launches (movegen launchers compiled for the host): every
+// workgroup of the grid in turn, its threads as host threads, one 64-lane
+// barrier per wave and one workgroup barrier; __shared__ variables become
+// function statics (the workgroups run one after another)
+#define __shared__ static
+struct dim3 {
+    unsigned x, y, z;
+    dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+#define hipSuccess 0
+#define hipDeviceAttributeMultiprocessorCount 0
+inline int emu_n_cu = 2;
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
+inline hipError_t hipDeviceGetAttribute(int* v, int attr, int dev) { (void)attr; (void)dev; *v = emu_n_cu; return hipSuccess; }
+template <class F> inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, F, int, size_t) {
+    *n = 1;
+    return hipSuccess;
+}
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
+namespace emu {
+template <class K, class... A> inline void launch(K kernel, unsigned g, unsigned nthreads, A... args) {
+    const unsigned nw = nthreads / 64;
+    grid = g;
+    block_threads = nthreads;
+    for (unsigned b = 0; b < g; ++b) {
+        std::vector<Wave> waves(nw);
+        std::vector<std::unique_ptr<std::barrier<>>> bars;
+        for (unsigned w = 0; w < nw; ++w) {
+            bars.emplace_back(new std::barrier<>(64));
+            waves[w].bar = bars.back().get();
+        }
+        std::barrier<> bb((std::ptrdiff_t)nthreads);
+        block_bar = &bb;
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nthreads; ++t)
+            th.emplace_back([&, t] {
+                tid = (int)t;
+                lane = (int)(t & 63u);
+                block = b;
+                cur = &waves[t >> 6];
+                kernel(args...);
+                // a thread that returns early must keep its wave's and the
+                // workgroup's barriers moving for the others
+                cur->bar->arrive_and_drop();
+                block_bar->arrive_and_drop();
+            });
+        for (auto& x : th) x.join();
+        block_bar = nullptr;
+    }
+}
+}  // namespace emu
+#define hipLaunchKernelGGL(kernel, g, b, shmem, stream, ...) emu::launch(kernel, dim3(g).x, dim3(b).x, __VA_ARGS__)

@@ -19,6 +19,7 @@ import os
 import shutil
 import subprocess
 
+import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,3 +40,75 @@ def test_board_major_doubles_equals_per_roll(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert '"mismatches": 0' in r.stdout, r.stdout[-2000:]
     assert '"board_major_roots": 0' not in r.stdout   # the board-major path actually ran
+
+
+def _build(tmp_path, src, name, defs=()):
+    exe = tmp_path / name
+    subprocess.run(["g++", "-std=c++20", "-O1", "-g", "-w", "-fsanitize=address", "-fno-omit-frame-pointer",
+                    *defs, "-I" + os.path.join(HERE, "cpuwave"),
+                    "-I" + os.path.join(REPO, "mlp-ppo-2ply-multi_amd", "csrc"),
+                    "-I" + os.path.join(REPO, "include"), "-x", "c++",
+                    os.path.join(HERE, "cpuwave", src), "-o", str(exe), "-pthread"],
+                   check=True, capture_output=True, text=True)
+    return exe
+
+
+def _unpack(w):
+    """packed rows uint32 [n, 8] -> uint8 [n, 52] (bgx_device.h packed_to_u8)"""
+    n = w.shape[0]
+    out = np.zeros((n, 52), np.uint8)
+    for k in range(6):
+        for q in range(8):
+            out[:, 8 * k + q] = (w[:, k] >> (4 * q)) & 15
+    for i in range(4):
+        out[:, 48 + i] = (w[:, 6] >> (4 * i)) & 15
+    return out
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_reply_launch_emulated_equals_oracle(tmp_path):
+    """The whole 2-ply reply launch as bgx_reply_moves issues it (reply kernel:
+    16-wave workgroups, sub-queue, per-roll calls; then the tier-2 block
+    kernel), emulated on the host under AddressSanitizer on self-play and random
+    positions: every (board, roll) list equals the oracle's movegen
+    (generate_all_moves.py:7-90), order included, for the default build and for
+    the board-major doubles build (BGX_DBL_BM=1), whose per-job output must be
+    byte-identical to the default's."""
+    orc = pytest.importorskip("oracle")
+    from test_gpu_parity import _fuzz_positions, _random_positions
+    pos = _fuzz_positions(11, 4) + _random_positions(12, 90)
+    boards = np.stack([p[0] for p in pos])
+    opp = np.array([p[1] for p in pos], np.uint8)
+    rows = np.zeros((len(pos), 9), np.uint32)
+    for k in range(6):
+        for q in range(8):
+            rows[:, k] |= boards[:, 8 * k + q].astype(np.uint32) << np.uint32(4 * q)
+    mover = 1 - opp.astype(np.uint32)
+    rows[:, 6] = (boards[:, 48].astype(np.uint32) | boards[:, 49].astype(np.uint32) << 4 |
+                  boards[:, 50].astype(np.uint32) << 8 | boards[:, 51].astype(np.uint32) << 12 | mover << 16)
+    rows[:, 8] = opp
+    pfile = tmp_path / "pos.bin"
+    rows.tofile(pfile)
+    env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0"}
+    dumps = []
+    for v in ("0", "1"):
+        exe = _build(tmp_path, "reply_emu.cpp", "reply_emu" + v, ["-DBGX_DBL_BM=" + v])
+        dump = tmp_path / ("dump" + v + ".bin")
+        r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(dump)], capture_output=True, text=True,
+                           timeout=900, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        dumps.append(dump.read_bytes())
+    assert dumps[0] == dumps[1]
+    d = np.frombuffer(dumps[0], np.int32)
+    at = 0
+    rolls = [(a, b) for a in range(1, 7) for b in range(a, 7)]
+    for i in range(len(pos)):
+        for a, b in rolls:
+            c = int(d[at])
+            at += 1
+            got = _unpack(d[at:at + 8 * max(c, 0)].view(np.uint32).reshape(-1, 8)) if c > 0 else np.zeros((0, 52))
+            at += 8 * max(c, 0)
+            n, res, _ = orc.movegen(boards[i], int(opp[i]), a, b, cap=4096)
+            assert c == n, (i, a, b, c, n)
+            np.testing.assert_array_equal(got, res[:n], err_msg=f"board {i} roll {a}-{b}")
+    assert at == d.shape[0]
