@@ -64,14 +64,42 @@ inline void sync() {
 #else
 inline void sync() { W().bar->arrive_and_wait(); }
 #endif
+// EMU_SITES: every exchange also checks that the 64 lanes reached it from the
+// same call site (build with -O0 -fno-inline so sites stay distinct): a
+// cross-lane operation under lane-divergent control flow reads inactive lanes
+// on the GPU, which this emulation would otherwise hide
+#ifdef EMU_SITES
+inline void* site_buf[32][64][8];
+inline int site_n[32][64];
+}  // namespace emu
+#include <cstdio>
+#include <execinfo.h>
+namespace emu {
+#endif
 // every lane's v (as 64-bit words)
-template <class T> inline void gather(T v, T* out) {
+template <class T> __attribute__((noinline)) inline void gather(T v, T* out) {
     static_assert(sizeof(T) <= 8, "scalar exchange");
     Wave& w = W();
     uint64_t u = 0;
     std::memcpy(&u, &v, sizeof(T));
     w.xbuf[lane] = u;
+#ifdef EMU_SITES
+    const int widx = cur ? tid >> 6 : 0;
+    site_n[widx][lane] = backtrace(site_buf[widx][lane], 8);   // the whole call chain (up to 8 frames)
+#endif
     sync();
+#ifdef EMU_SITES
+    if (lane == 0)
+        for (int i = 1; i < 64; ++i)
+            if (site_n[widx][i] != site_n[widx][0] ||
+                std::memcmp(site_buf[widx][i], site_buf[widx][0], sizeof(void*) * site_n[widx][0])) {
+                fprintf(stderr, "EMU_SITES: lanes 0 and %d of wave %d exchange at different call chains:\n", i, widx);
+                for (int k = 0; k < 8; ++k)
+                    fprintf(stderr, "  %p %p\n", k < site_n[widx][0] ? site_buf[widx][0][k] : nullptr,
+                            k < site_n[widx][i] ? site_buf[widx][i][k] : nullptr);
+                std::abort();
+            }
+#endif
     for (int i = 0; i < 64; ++i) std::memcpy(&out[i], &w.xbuf[i], sizeof(T));
     sync();
 }

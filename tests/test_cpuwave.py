@@ -112,3 +112,48 @@ def test_reply_launch_emulated_equals_oracle(tmp_path):
             assert c == n, (i, a, b, c, n)
             np.testing.assert_array_equal(got, res[:n], err_msg=f"board {i} roll {a}-{b}")
     assert at == d.shape[0]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_reply_launch_cross_lane_ops_are_uniform(tmp_path):
+    """Every cross-lane operation of the reply launch (ballot, shuffles,
+    readlane, DPP scans) is reached by all 64 lanes of the wave from the same
+    call chain (EMU_SITES build, -O0 -fno-inline): on the GPU one under
+    lane-divergent control flow would read inactive lanes. Both builds
+    (default, board-major doubles); the emulation itself aborts on a kernel
+    that branches around a shuffle (checked with a deliberately divergent one)."""
+    from test_gpu_parity import _random_positions
+    pytest.importorskip("oracle")
+    pos = _random_positions(21, 40)
+    boards = np.stack([p[0] for p in pos])
+    opp = np.array([p[1] for p in pos], np.uint8)
+    rows = np.zeros((len(pos), 9), np.uint32)
+    for k in range(6):
+        for q in range(8):
+            rows[:, k] |= boards[:, 8 * k + q].astype(np.uint32) << np.uint32(4 * q)
+    rows[:, 6] = (boards[:, 48].astype(np.uint32) | boards[:, 49].astype(np.uint32) << 4 |
+                  boards[:, 50].astype(np.uint32) << 8 | boards[:, 51].astype(np.uint32) << 12 |
+                  (1 - opp.astype(np.uint32)) << 16)
+    rows[:, 8] = opp
+    pfile = tmp_path / "pos.bin"
+    rows.tofile(pfile)
+    inc = ["-I" + os.path.join(HERE, "cpuwave"), "-I" + os.path.join(REPO, "mlp-ppo-2ply-multi_amd", "csrc"),
+           "-I" + os.path.join(REPO, "include")]
+    bad = tmp_path / "bad.cpp"
+    bad.write_text('#include "hip/hip_runtime.h"\n'
+                   "__global__ void k(int* o) { int v = (int)threadIdx.x; int r;\n"
+                   "  if (threadIdx.x & 1) r = __shfl(v, 0, 64); else r = __shfl(v, 1, 64); o[threadIdx.x] = r; }\n"
+                   "int main() { static int o[64]; hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, nullptr, o); }\n")
+    exe = tmp_path / "bad"
+    subprocess.run(["g++", "-std=c++20", "-O0", "-fno-inline", "-g", "-w", "-DEMU_SITES", *inc, "-x", "c++", str(bad),
+                    "-o", str(exe), "-pthread"], check=True, capture_output=True, text=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "EMU_SITES" in r.stderr
+    for v in ("0", "1"):
+        exe = tmp_path / ("site" + v)
+        subprocess.run(["g++", "-std=c++20", "-O0", "-fno-inline", "-g", "-w", "-DEMU_SITES", "-DBGX_DBL_BM=" + v, *inc,
+                        "-x", "c++", os.path.join(HERE, "cpuwave", "reply_emu.cpp"), "-o", str(exe), "-pthread"],
+                       check=True, capture_output=True, text=True)
+        r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(tmp_path / ("s" + v))], capture_output=True,
+                           text=True, timeout=900)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
