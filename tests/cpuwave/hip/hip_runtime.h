@@ -26,15 +26,17 @@
 typedef int hipError_t;
 typedef void* hipStream_t;
 
-struct uint4 { uint32_t x, y, z, w; };
+struct alignas(16) uint4 { uint32_t x, y, z, w; };
 inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return {x, y, z, w}; }
 struct emu_dim3 { unsigned x, y, z; };
+struct alignas(16) float4 { float x, y, z, w; };
+struct float2 { float x, y; };
 
 namespace emu {
 // one emulated wavefront: its exchange buffer and its 64-lane barrier
 struct Wave {
     std::barrier<>* bar = nullptr;
-    uint64_t xbuf[64];
+    alignas(16) unsigned char xbuf[64][64];
 };
 inline thread_local int lane = 0;          // lane in the wave
 inline thread_local int tid = 0;           // thread in the workgroup
@@ -78,11 +80,9 @@ namespace emu {
 #endif
 // every lane's v (as 64-bit words)
 template <class T> __attribute__((noinline)) inline void gather(T v, T* out) {
-    static_assert(sizeof(T) <= 8, "scalar exchange");
+    static_assert(sizeof(T) <= 64, "exchange of at most 64 bytes per lane");
     Wave& w = W();
-    uint64_t u = 0;
-    std::memcpy(&u, &v, sizeof(T));
-    w.xbuf[lane] = u;
+    std::memcpy(w.xbuf[lane], &v, sizeof(T));
 #ifdef EMU_SITES
     const int widx = cur ? tid >> 6 : 0;
     site_n[widx][lane] = backtrace(site_buf[widx][lane], 8);   // the whole call chain (up to 8 frames)
@@ -100,7 +100,7 @@ template <class T> __attribute__((noinline)) inline void gather(T v, T* out) {
                 std::abort();
             }
 #endif
-    for (int i = 0; i < 64; ++i) std::memcpy(&out[i], &w.xbuf[i], sizeof(T));
+    for (int i = 0; i < 64; ++i) std::memcpy(&out[i], w.xbuf[i], sizeof(T));
     sync();
 }
 template <class T> inline T lane_value(T v, int k) {
@@ -225,8 +225,11 @@ template <class F> inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocesso
 }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
 namespace emu {
-template <class K, class... A> inline void launch(K kernel, unsigned g, unsigned nthreads, A... args) {
+inline void* dyn_lds = nullptr;   // the workgroup's dynamic LDS (extern __shared__ arrays)
+template <class K, class... A> inline void launch(K kernel, unsigned g, unsigned nthreads, size_t shmem, A... args) {
     const unsigned nw = nthreads / 64;
+    std::vector<unsigned long long> dyn((shmem + 7) / 8 + 1);
+    dyn_lds = dyn.data();
     grid = g;
     block_threads = nthreads;
     for (unsigned b = 0; b < g; ++b) {
@@ -254,6 +257,41 @@ template <class K, class... A> inline void launch(K kernel, unsigned g, unsigned
         for (auto& x : th) x.join();
         block_bar = nullptr;
     }
+    dyn_lds = nullptr;
 }
 }  // namespace emu
-#define hipLaunchKernelGGL(kernel, g, b, shmem, stream, ...) emu::launch(kernel, dim3(g).x, dim3(b).x, __VA_ARGS__)
+#define hipLaunchKernelGGL(kernel, g, b, shmem, stream, ...) \
+    emu::launch(kernel, dim3(g).x, dim3(b).x, (size_t)(shmem), __VA_ARGS__)
+
+// ---- MLP kernels: math builtins, LDS-DMA, MFMA (clang host builds: ext_vector_type, _Float16)
+#define __builtin_amdgcn_exp2f(x) std::exp2((float)(x))
+#define __builtin_amdgcn_rcpf(x) (1.0f / (float)(x))
+#define __builtin_amdgcn_sched_barrier(n) ((void)0)
+#define __builtin_amdgcn_s_waitcnt(n) ((void)0)
+#define __builtin_amdgcn_s_setprio(n) ((void)0)
+// global -> LDS, size bytes per lane: lane l's bytes land at the (wave-uniform)
+// LDS address + l * size
+#define __builtin_amdgcn_global_load_lds(g, l, size, off, aux) \
+    std::memcpy((char*)(void*)(l) + (size_t)emu::lane * (size), (const void*)(g), (size))
+// v_mfma_f32_32x32x16_f16: D[i][j] = C[i][j] + sum_k A[i][k] B[k][j] (i, j < 32, k < 16);
+// lane l holds A[l % 32][8 (l / 32) + e] and B[8 (l / 32) + e][l % 32] (e < 8), and
+// D[8 (r / 4) + 4 (l / 32) + r % 4][l % 32] in accumulator register r
+template <class HA, class HB, class FC> inline FC emu_mfma_32x32x16(HA a, HB b, FC c) {
+    HA A[64];
+    HB B[64];
+    emu::gather(a, A);
+    emu::gather(b, B);
+    const int l = emu::lane, j = l & 31;
+    FC d;
+    for (int r = 0; r < 16; ++r) {
+        const int i = 8 * (r >> 2) + 4 * (l >> 5) + (r & 3);
+        float acc = 0.0f;
+        for (int k = 0; k < 16; ++k) acc += (float)A[i + 32 * (k >> 3)][k & 7] * (float)B[j + 32 * (k >> 3)][k & 7];
+        d[r] = c[r] + acc;
+    }
+    return d;
+}
+#define __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, x, y, z) emu_mfma_32x32x16((a), (b), (c))
+#define hipFuncAttributeMaxDynamicSharedMemorySize 0
+#define hipErrorInvalidValue 1
+template <class F> inline hipError_t hipFuncSetAttribute(F, int, int) { return hipSuccess; }

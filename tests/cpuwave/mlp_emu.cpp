@@ -1,0 +1,61 @@
+// tests/cpuwave/mlp_emu.cpp -- test infrastructure (host build, emulated workgroups).
+// The MLP launch (bgx_launch_mlp, bgx_mlp.hip: LUT feature build, split-fp16
+// MFMA tiles, canonical epilogue) on the host: the kernels' source (a copy
+// with the inline-asm scheduling hints removed and the dynamic LDS array
+// bound to the emulated workgroup's buffer) against
+// tests/cpuwave/hip/hip_runtime.h, whose v_mfma_f32_32x32x16_f16 follows the
+// operand layout the fragments are built for (bgx_frag.h).
+// Usage: mlp_emu rows.bin weights.bin nt out.bin
+//   rows: n x 8 packed words (uint32); weights: W1 [128][198], b1 [128],
+//   w2 [128], b2 [1] (float32); nt 1 or 2 (the launcher's two kernels);
+//   out: n float32 V
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "bgx_frag.h"
+#include "bgx_mlp.hip"
+
+static_assert(bgx_frag::NFRAG == bgx::NFRAG, "fragment count");
+
+int main(int argc, char** argv) {
+    if (argc < 5) return 2;
+    std::vector<uint32_t> rows;
+    {
+        FILE* f = fopen(argv[1], "rb");
+        if (!f) return 2;
+        uint32_t v[8];
+        while (fread(v, 4, 8, f) == 8) rows.insert(rows.end(), v, v + 8);
+        fclose(f);
+    }
+    std::vector<float> w(128 * 198 + 128 + 128 + 1);
+    {
+        FILE* f = fopen(argv[2], "rb");
+        if (!f || fread(w.data(), 4, w.size(), f) != w.size()) return 2;
+        fclose(f);
+    }
+    const float* W1 = w.data();
+    const float* b1 = W1 + 128 * 198;
+    const float* w2 = b1 + 128;
+    const float b2 = w2[128];
+    std::vector<uint16_t> frag;
+    const int e = bgx_frag::build_fragments(W1, b1, frag);
+    const int n = (int)rows.size() / 8;
+    std::vector<float> out(n, -12345.0f);
+    bgx::MlpArgs a{};
+    a.rows = rows.data();
+    a.n_rows = n;
+    a.n_max = n;
+    a.nt = atoi(argv[3]);
+    a.out = out.data();
+    a.wfrag = (const uint4*)frag.data();
+    a.rowc = w2;
+    a.b2 = b2;
+    a.feat_scale = (float)std::ldexp(1.0, -e);
+    if (bgx_launch_mlp(&a, nullptr) != hipSuccess) return 3;
+    FILE* f = fopen(argv[4], "wb");
+    if (!f) return 2;
+    fwrite(out.data(), 4, out.size(), f);
+    fclose(f);
+    return 0;
+}

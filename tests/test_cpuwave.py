@@ -24,6 +24,26 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+def _emu_sources(tmp_path):
+    """A copy of csrc/ for host builds: the inline-asm scheduling hints
+    (`asm volatile(...)`: waitcnts, register pins) removed and each dynamic LDS
+    array (`extern __shared__ T x[];`) bound to the emulated workgroup's buffer.
+    The kernels' code is otherwise the product's, unchanged."""
+    import glob
+    import re
+    d = tmp_path / "csrc_emu"
+    d.mkdir(exist_ok=True)
+    for f in glob.glob(os.path.join(REPO, "mlp-ppo-2ply-multi_amd", "csrc", "*.h")) + \
+            glob.glob(os.path.join(REPO, "mlp-ppo-2ply-multi_amd", "csrc", "*.hip")):
+        s = open(f).read()
+        s = re.sub(r"asm volatile\((?:[^;])*?\);", ";", s)
+        s = re.sub(r"extern __shared__ (?:__attribute__\(\(aligned\(\d+\)\)\) )?([\w ]+?) (\w+)\[\];",
+                   r"\1* \2 = (\1*)emu::dyn_lds;", s)
+        (d / os.path.basename(f)).write_text(s)
+    return d
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
@@ -157,3 +177,50 @@ def test_reply_launch_cross_lane_ops_are_uniform(tmp_path):
         r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(tmp_path / ("s" + v))], capture_output=True,
                            text=True, timeout=900)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def _pack(boards, flag):
+    rows = np.zeros((len(boards), 8), np.uint32)
+    for k in range(6):
+        for q in range(8):
+            rows[:, k] |= boards[:, 8 * k + q].astype(np.uint32) << np.uint32(4 * q)
+    rows[:, 6] = (boards[:, 48].astype(np.uint32) | boards[:, 49].astype(np.uint32) << 4 |
+                  boards[:, 50].astype(np.uint32) << 8 | boards[:, 51].astype(np.uint32) << 12 |
+                  np.asarray(flag).astype(np.uint32) << 16)
+    return rows
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="no ROCm clang")
+def test_mlp_kernels_emulated_equal_oracle_value(tmp_path):
+    """The MLP launch (bgx_launch_mlp: the 16-wave single-tile kernel and the
+    8-wave interleaved-epilogue kernel), emulated on the host with the
+    v_mfma_f32_32x32x16_f16 operand layout, gives the oracle's fp64 value
+    (policy_network.py:53-70) within 1e-6 on the shipped checkpoint for random
+    placements (bar, borne-off checkers): the fragment layout (bgx_frag.h), the
+    LUT features, the split-fp16 product and the epilogue, checked without a
+    GPU. AddressSanitizer on."""
+    orc = pytest.importorskip("oracle")
+    from test_gpu_parity import _random_positions
+    pos = _random_positions(3, 150)
+    boards = np.stack([p[0] for p in pos])
+    pl = np.array([p[1] for p in pos])
+    _pack(boards, pl).tofile(tmp_path / "rows.bin")
+    w = np.load(os.path.join(HERE, "golden", "weights_ckpt2100000.npz"))
+    W = {k: w[k].astype(np.float32) for k in ("W1", "b1", "w2", "b2")}
+    np.concatenate([W[k].ravel() for k in ("W1", "b1", "w2", "b2")]).astype(np.float32).tofile(tmp_path / "w.bin")
+    ref = orc.value(W, orc.encode_many(boards, pl))
+    src = _emu_sources(tmp_path)
+    exe = tmp_path / "mlp_emu"
+    subprocess.run([CLANG, "-std=c++20", "-O1", "-g", "-w", "-fsanitize=address", "-fno-omit-frame-pointer",
+                    "-I" + str(src), "-I" + os.path.join(HERE, "cpuwave"), "-I" + os.path.join(REPO, "include"),
+                    "-x", "c++", os.path.join(HERE, "cpuwave", "mlp_emu.cpp"), "-o", str(exe), "-pthread"],
+                   check=True, capture_output=True, text=True)
+    env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0"}
+    for nt in ("1", "2"):
+        out = tmp_path / ("v" + nt + ".bin")
+        r = subprocess.run([str(exe), str(tmp_path / "rows.bin"), str(tmp_path / "w.bin"), nt, str(out)],
+                           capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        v = np.fromfile(out, np.float32)
+        assert v.shape == ref.shape
+        assert np.abs(v - ref).max() < 1e-6, (nt, np.abs(v - ref).max())
