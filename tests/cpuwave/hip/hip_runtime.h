@@ -218,7 +218,14 @@ struct dim3 {
 inline int emu_n_cu = 2;
 inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
-inline hipError_t hipDeviceGetAttribute(int* v, int attr, int dev) { (void)attr; (void)dev; *v = emu_n_cu; return hipSuccess; }
+// EMU_N_CU: the emulated compute units (grid sizes of the persistent launchers; default 2)
+inline hipError_t hipDeviceGetAttribute(int* v, int attr, int dev) {
+    (void)attr;
+    (void)dev;
+    const char* e = getenv("EMU_N_CU");
+    *v = e ? atoi(e) : emu_n_cu;
+    return hipSuccess;
+}
 template <class F> inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, F, int, size_t) {
     *n = 1;
     return hipSuccess;
