@@ -291,7 +291,9 @@ int bgx_copy_async(void* dst, const void* src, uint64_t bytes, int kind, void* s
  * made d_src ready, e.g. by bgx_harvest_fetch) and *ticket identifies it;
  * bgx_dma_wait(ticket, timeout_ms <= 0: no limit) waits for it and releases the
  * ticket (exactly once per ticket). BGX_E_STATE when the device has no DMA
- * engine for the direction. */
+ * engine for the direction, or when the wait times out: the copy is then still
+ * in flight, the ticket stays valid (wait again) and both buffers must stay
+ * allocated until a wait succeeds. */
 int bgx_dma_copy_d2h(void* h_dst, const void* d_src, uint64_t bytes, int device, uint64_t* ticket);
 int bgx_dma_wait(uint64_t ticket, int timeout_ms);
 

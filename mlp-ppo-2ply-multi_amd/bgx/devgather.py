@@ -30,6 +30,22 @@ from .hostgather import EP_BYTES, REC_BYTES, HostGather, Pending, make_tag, slot
 from .records import EP_WORDS, REC_WORDS
 
 
+def pci_location(index: int):
+    """(PCI domain, bus, device) of this process's GPU `index`."""
+    p = torch.cuda.get_device_properties(index)
+    return int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)
+
+
+def device_by_pci(loc) -> int:
+    """This process's ordinal of the GPU at PCI location `loc`."""
+    loc = tuple(int(x) for x in loc)
+    for i in range(torch.cuda.device_count()):
+        if pci_location(i) == loc:
+            return i
+    raise RuntimeError(f"DeviceGather: the trainer rank's GPU (PCI {loc[0]:04x}:{loc[1]:02x}:{loc[2]:02x}) is not "
+                       "visible to this process (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES): a peer copy needs it")
+
+
 class DeviceGather(HostGather):
     """One per rank. dst holds the slots ([world][2][slot_bytes] on its GPU);
     the control words are HostGather's header-only segments."""
@@ -49,17 +65,23 @@ class DeviceGather(HostGather):
 
     # ---- setup (collective once, see setup())
     def export(self):
-        """dst: (IPC handle, offset, dst's device ordinal) of its slots."""
+        """dst: (IPC handle, offset, PCI location of dst's GPU) of its slots. The
+        GPU travels as its PCI (domain, bus, device), not as an ordinal: an
+        ordinal names the same GPU in two processes only when both see the
+        same device list (per-rank HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES
+        renumber it)."""
         from ._lib import check, lib
         h = (ctypes.c_uint8 * 64)()
         off = ctypes.c_uint64(0)
         check(lib().bgx_ipc_export(self.buf.data_ptr(), h, ctypes.byref(off)), "bgx_ipc_export")
-        return bytes(h), int(off.value), self.dev_index
+        return bytes(h), int(off.value), pci_location(self.dev_index)
 
     def open(self, info):
-        """Peer: map dst's slots into this process."""
+        """Peer: map dst's slots into this process; dst's GPU is found in this
+        process's device list by its PCI location."""
         from ._lib import check, lib
-        handle, off, dst_dev = info
+        handle, off, loc = info
+        dst_dev = device_by_pci(loc)
         with torch.cuda.device(self.device):
             p = ctypes.c_void_p(0)
             check(lib().bgx_ipc_open((ctypes.c_uint8 * 64).from_buffer_copy(handle), off, ctypes.byref(p)),
@@ -75,6 +97,8 @@ class DeviceGather(HostGather):
         slot on dst's GPU (ready: as HostGather.publish)."""
         from ._lib import check, lib
         n_eps, n_recs = h.n_episodes, h.n_records
+        if self.broken:
+            raise RuntimeError("DeviceGather: an earlier DMA copy did not finish; its slot is still owned by it")
         need = n_eps * EP_BYTES + n_recs * REC_BYTES
         if need > self.slot_bytes:   # before the batch number moves: dst still waits for the same batch
             raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")
@@ -114,9 +138,17 @@ class DeviceGather(HostGather):
             hdr = raw[:n_eps * EP_BYTES].view(torch.int32).view(-1, EP_WORDS)
             rec = raw[n_eps * EP_BYTES:].view(torch.int32).view(-1, REC_WORDS)
             if copy:
-                hdr, rec = hdr.clone(), rec.clone()
-                c[5] = seq   # acknowledged: the peer may reuse this slot
+                with torch.cuda.device(self.device):
+                    hdr, rec = hdr.clone(), rec.clone()
             out.append((hdr, rec))
+        if copy:
+            # the clones run on dst's current stream, possibly queued behind its own
+            # persistent launch: they must have READ the slots before a peer is told
+            # it may overwrite them (its next publish is an SDMA write into the slot)
+            torch.cuda.current_stream(self.device).synchronize()
+            for r in range(self.world):
+                if r != self.dst:
+                    self.ctrl[r][5] = seq   # acknowledged: the peer may reuse this slot
         return out
 
     def close(self):

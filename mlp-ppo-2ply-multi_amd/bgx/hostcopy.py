@@ -25,6 +25,7 @@ class Staging:
         self.mm = None
         self.buf = None
         self.addr = None
+        self.broken = False   # a copy timed out (copy()): its buffer is never reused
 
     def _ensure(self, nbytes: int):
         if nbytes <= self.size:
@@ -42,6 +43,8 @@ class Staging:
         """(headers uint32 [n, 16], records uint32 [m, 12]) of a Harvest whose
         device arrays are complete (harvest_fetch waited for them)."""
         from ._lib import check, lib
+        if self.broken:
+            raise RuntimeError("Staging: an earlier DMA copy did not finish; its buffer is still owned by it")
         ne, nr = h.n_episodes, h.n_records
         hb, rb = ne * EP_WORDS * 4, nr * REC_WORDS * 4
         if ne == 0:
@@ -52,8 +55,19 @@ class Staging:
               "bgx_dma_copy_d2h")
         check(lib().bgx_dma_copy_d2h(self.addr + hb, h.records.data_ptr(), rb, self.device, ctypes.byref(t2)),
               "bgx_dma_copy_d2h")
-        check(lib().bgx_dma_wait(t1.value, timeout_ms), "bgx_dma_wait")
-        check(lib().bgx_dma_wait(t2.value, timeout_ms), "bgx_dma_wait")
+        from ._lib import BgxError
+        try:
+            check(lib().bgx_dma_wait(t1.value, timeout_ms), "bgx_dma_wait")
+            check(lib().bgx_dma_wait(t2.value, timeout_ms), "bgx_dma_wait")
+        except BgxError:
+            # a copy still in flight owns the staging buffer and the harvest's
+            # arrays: keep both for the life of the process, refuse further copies
+            from .hostgather import STUCK_COPIES
+            STUCK_COPIES.append((self.mm, self.buf, h))
+            self.mm = self.buf = self.addr = None
+            self.size = 0
+            self.broken = True
+            raise
         hdr = self.buf[:hb].view(np.uint32).reshape(ne, EP_WORDS)
         rec = self.buf[hb:hb + rb].view(np.uint32).reshape(nr, REC_WORDS)
         return hdr, rec

@@ -64,6 +64,12 @@ def slot_bytes_for(lanes: int, steps_per_harvest: int, max_steps: int = 300) -> 
     return ((recs * REC_BYTES + eps * EP_BYTES) + 4095) & ~4095
 
 
+# batches whose DMA copy did not finish within its timeout: kept referenced (with
+# their source arrays) for the life of the process, since the engine may still
+# read and write their memory (bgx_dma_wait leaves such a copy in flight)
+STUCK_COPIES = []
+
+
 class Pending:
     """A batch in flight. It holds the source arrays (`keep`) until wait()
     has seen the copies finish: the caller may drop its Harvest at once, and
@@ -79,9 +85,18 @@ class Pending:
         if self.event is not None:
             self.event.synchronize()
         if self.dma:
-            from ._lib import check, lib
-            for t in self.dma:
-                check(lib().bgx_dma_wait(t, int(self.g.timeout * 1000)), "bgx_dma_wait")
+            from ._lib import BgxError, check, lib
+            for i, t in enumerate(self.dma):
+                try:
+                    check(lib().bgx_dma_wait(t, int(self.g.timeout * 1000)), "bgx_dma_wait")
+                except BgxError:
+                    # the copy may still be running: its source blocks and the
+                    # destination slot stay owned by it for the life of the
+                    # process, and the gather refuses further batches
+                    self.dma = self.dma[i:]
+                    STUCK_COPIES.append(self)
+                    self.g.broken = True
+                    raise
             self.dma = ()
         self.keep = None
         c = self.g.ctrl[self.g.rank]
@@ -127,6 +142,7 @@ class HostGather:
         self.timeout = timeout
         self.device = device
         self.seq = 0
+        self.broken = False   # a DMA copy of this gather timed out (Pending.wait): no further batches
         self._mine = _Segment(self._name(rank), size=HDR + 2 * self.slot_bytes)
         self.shm = {rank: self._mine}
         np.ndarray((8,), np.int64, buffer=self._mine.buf[:HDR])[:] = 0
@@ -204,6 +220,8 @@ class HostGather:
         ready=True: the harvest's device arrays are complete (bgx_harvest_fetch
         waited for them); otherwise the current stream is synchronized first."""
         n_eps, n_recs = h.n_episodes, h.n_records
+        if self.broken:
+            raise RuntimeError("HostGather: an earlier DMA copy did not finish; its slot is still owned by it")
         need = n_eps * EP_BYTES + n_recs * REC_BYTES
         if need > self.slot_bytes:   # before the batch number moves: dst still waits for the same batch
             raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")

@@ -603,6 +603,9 @@ int bgx_dma_wait(uint64_t ticket, int timeout_ms) {
         hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, spin_ns, HSA_WAIT_STATE_ACTIVE);
         if (v >= 1 && ns > spin_ns)
             v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, ns - spin_ns, HSA_WAIT_STATE_BLOCKED);
+        // past the timeout the copy is still in flight: the ticket stays valid (a
+        // later wait may see it end; its signal is destroyed then) and the caller
+        // must keep both buffers alive (bgx/hostgather.py STUCK_COPIES)
         if (v >= 1) return fail(BGX_E_STATE, "bgx_dma_wait: copy not finished after %d ms", timeout_ms);
         hsa_signal_destroy(sig);
         return BGX_OK;

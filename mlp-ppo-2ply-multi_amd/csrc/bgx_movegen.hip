@@ -251,8 +251,16 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         }
         if (k >= nk) {
             // no items left for this wave: done once every item is done (no more
-            // pushes) and the sub-queue is drained
-            if (lds_ld(&items_done) >= nk && lds_ld(&sub_head) >= lds_ld(&sub_res)) break;
+            // pushes) and the sub-queue is drained. Lane 0 reads the three counters
+            // and the verdict is broadcast: the exit is wave-uniform by
+            // construction, not by the hardware returning one LDS word to every
+            // lane (acquire pairs with the release increment of items_done below,
+            // so a drained verdict sees every push of every finished item)
+            int fin = 0;
+            if (l == 0)
+                fin = __hip_atomic_load(&items_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= nk &&
+                      lds_ld(&sub_head) >= lds_ld(&sub_res);
+            if (uniform(fin)) break;
             if (++spin >= (1u << 24)) {
                 if (l == 0) atomicOr(a.err_flags, BGX_ERRF_WAIT_BOUND);
                 break;
@@ -343,7 +351,11 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                 }
             }
         }
-        if (l == 0) atomicAdd(&items_done, 1);
+        // release: the item's sub-queue stores (lanes < 15, above) are ordered
+        // before the count that lets waves leave (the wave's LDS stores are
+        // complete at the fence this emits)
+        wave_sync();
+        if (l == 0) __hip_atomic_fetch_add(&items_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         k = kn;
     }
 }

@@ -9,8 +9,10 @@ GPU and putting every finished Episode on the queue exactly as
 play_episode/run do (worker.py:47-76). Each cycle queues the next launch and
 its harvest before the host reads the previous harvest (harvest_enqueue /
 harvest_fetch), so the GPUs keep stepping while the host copies and queues.
-Parameters are re-read when the version advances (worker.py:66-76), at every
-harvest.
+Parameters are re-read when the version advances (worker.py:66-76), at the
+start of every cycle, before its launch is queued: a new version steers the
+very next launch (set_weights waits for the launch in flight, so an update
+costs one pipeline drain, and only when the version moved).
 
 Knobs (environment): BGX_WORKERS (7: main.py:86's worker count),
 BGX_GPU_MAP (explicit GPUs per worker id: "0;1;2;3;4;5;6,7" = worker 6 drives
@@ -108,6 +110,7 @@ class Worker:
         are views into the engines' buffers, valid until the next cycle
         queues its tickets; the first cycle returns none."""
         engines = self._ensure_engine()
+        self._maybe_update()   # before the launch is queued: no launch runs on stale weights
         tickets = []
         for e in engines:
             with torch.cuda.device(e.device):
@@ -124,8 +127,11 @@ class Worker:
         """Advance all lanes one launch and return the Episodes of the previous
         launch's harvest (already to_numpy()'d)."""
         out = []
-        for h in self._step_all(steps):
-            out += to_episodes(h, Episode, Experience, Player)
+        for e, h in zip(self.engines, self._step_all(steps)):
+            # on the harvest's own device: its decode kernels and the .cpu() that
+            # follows use that device's current stream
+            with torch.cuda.device(e.device):
+                out += to_episodes(h, Episode, Experience, Player)
         return out
 
     def harvest_records(self, steps=None):
@@ -164,7 +170,6 @@ class Worker:
             else:
                 for episode in self.play_episodes():
                     self.experience_queue.put(episode)
-            self._maybe_update()
             while self.experience_queue.qsize() > self.max_pending:
                 time.sleep(0.01)
                 self._maybe_update()

@@ -95,7 +95,7 @@ def test_gloo_world2_gathers_real_harvests(weights_seed0):
     assert total > 100
 
 
-def _hg_rank(rank, world, port, L, steps, out, mode="host"):
+def _hg_rank(rank, world, port, L, steps, out, mode="host", chunks=None, busy=False):
     import sys
     from conftest import PKG, golden
     sys.path.insert(0, PKG)
@@ -114,10 +114,19 @@ def _hg_rank(rank, world, port, L, steps, out, mode="host"):
     e = Engine(lanes=n, lane_base=base, seed=17)
     e.set_weights(w, 1.5, 1)
     got, pend = [], None
-    for seq, chunk in enumerate((steps // 2, steps - steps // 2), start=1):
+    for seq, chunk in enumerate(chunks or (steps // 2, steps - steps // 2), start=1):
         e.step(chunk)
         h = e.harvest()
         if rank == 0:
+            if busy:
+                # rank 0's stream busy when it collects: the slot clones queue behind
+                # ~30 ms of work, and the peer may overwrite a slot only after they ran
+                try:
+                    torch.cuda._sleep(80_000_000)
+                except (AttributeError, RuntimeError):
+                    a = torch.ones((4096, 4096), device="cuda")
+                    for _ in range(20):
+                        a = (a @ a) * 0.0
             parts = g.collect(seq)
             if mode == "device":   # device tensors on rank 0's GPU
                 assert all(p is None or (p[0].is_cuda and p[1].is_cuda) for p in parts)
@@ -149,14 +158,19 @@ def test_host_gather_world2_real_harvests(weights_seed0, mode):
     handed over by SCM_RIGHTS) by the SDMA engines (bgx_dma_copy_d2h); merged
     == one Engine over both lane blocks. mode "device" (bench.py --gather
     device, bgx/devgather.py): rank 1 copies into slots on rank 0's GPU memory,
-    opened by IPC, with bgx_dma_copy_d2d; rank 0 gets device tensors."""
+    opened by IPC, with bgx_dma_copy_d2d; rank 0 gets device tensors. The
+    device mode runs 6 batches (each of the two slots per rank reused three
+    times) with rank 0's stream kept busy while it collects, so a slot
+    acknowledged before its clone ran would be overwritten."""
     from bgx import Engine
     from bgx.records import episode_bounds
     L, steps = 128, 240
+    chunks = (40,) * 6 if mode == "device" else None   # device: 6 batches, each slot reused three times
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_hg_rank, args=(r, 2, port, L, steps, q, mode)) for r in range(2)]
+    procs = [ctx.Process(target=_hg_rank, args=(r, 2, port, L, steps, q, mode, chunks, mode == "device"))
+             for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
@@ -166,7 +180,7 @@ def test_host_gather_world2_real_harvests(weights_seed0, mode):
     e = Engine(lanes=2 * L, seed=17)
     e.set_weights(weights_seed0, 1.5, 1)
     want = []
-    for chunk in (steps // 2, steps - steps // 2):
+    for chunk in chunks or (steps // 2, steps - steps // 2):
         e.step(chunk)
         h = e.harvest()
         want.append((h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32)))
@@ -176,12 +190,13 @@ def test_host_gather_world2_real_harvests(weights_seed0, mode):
         offs, _ = episode_bounds(hdr)
         return {(int(r[0]), int(r[1])): (r.copy(), rec[offs[i]:offs[i + 1]]) for i, r in enumerate(hdr)}
 
+    assert len(got) == len(want)
     for parts, (wh, wr) in zip(got, want):
         merged = {}
         for hh, rr in parts:
             merged.update(by_episode(hh, rr))
         ref = by_episode(wh, wr)
-        assert merged.keys() == ref.keys() and len(ref) > 20
+        assert merged.keys() == ref.keys() and len(ref) > (0 if chunks else 20)
         for key in ref:
             np.testing.assert_array_equal(merged[key][0], ref[key][0], err_msg=str(key))
             np.testing.assert_array_equal(merged[key][1], ref[key][1], err_msg=str(key))

@@ -69,3 +69,61 @@ def test_main_loop_delivers_reference_episodes(weights_seed0, monkeypatch):
         assert ep.win_type in (None, "regular", "gammon", "backgammon")
         assert (ep.win_type is None) == (not bool(xs[-1].done.item()))
     assert n_exp > 1000
+
+
+class _PM:
+    """ParameterManager stand-in (get_parameters / get_version / get_temperature)."""
+
+    def __init__(self, w, version=1):
+        self.w, self.v = w, version
+
+    def get_parameters(self):
+        return self.w
+
+    def get_version(self):
+        return self.v
+
+    def get_temperature(self):
+        return 1.5
+
+
+def test_pipelined_worker_matches_engine(weights_seed0, monkeypatch):
+    """multi/worker.py's pipelined cycle (each call queues the next launch and
+    returns the previous launch's harvest) hands over exactly the engine's own
+    harvests, one cycle late: call k's arrays equal a plain Engine's harvest
+    after launch k - 1 (same seed, lanes and lane base as the worker's GPU 0),
+    the first call returns none, and a version bump before a cycle steers that
+    cycle's launch (the direct engine takes the new weights at the same point)."""
+    from multi.worker import Worker
+    from bgx import Engine
+    monkeypatch.setenv("BGX_GPU_MAP", "0")
+    monkeypatch.setenv("BGX_LANES", "96")
+    monkeypatch.setenv("BGX_BALANCE", "0")        # lockstep launches: the harvests are run-independent
+    monkeypatch.setenv("BGX_STEPS_PER_HARVEST", "60")
+    w2 = {k: (v * 0.5 if k == "W1" else v) for k, v in weights_seed0.items()}
+    pm = _PM(weights_seed0)
+    wk = Worker(0, pm, None)
+    got = []
+    for k in range(5):
+        if k == 3:
+            pm.w, pm.v = w2, 2
+        hdr, rec = wk.harvest_records()
+        got.append((hdr.copy(), rec.copy()))
+    torch.cuda.set_device(0)
+    e = Engine(lanes=96, seed=1000003, lane_base=0, balance=False)
+    e.set_weights(weights_seed0, temperature=1.5, version=1)
+    want = []
+    for k in range(4):
+        if k == 3:
+            e.set_weights(w2, temperature=1.5, version=2)
+        e.step(60)
+        h = e.harvest()
+        want.append((h.headers.cpu().numpy().view(np.uint32), h.records.cpu().numpy().view(np.uint32)))
+    e.close()
+    for e_ in wk.engines:
+        e_.close()
+    assert got[0][0].shape[0] == 0 and got[0][1].shape[0] == 0   # nothing finished before the first launch
+    for k in range(4):
+        np.testing.assert_array_equal(got[k + 1][0], want[k][0], err_msg=f"headers of launch {k}")
+        np.testing.assert_array_equal(got[k + 1][1], want[k][1], err_msg=f"records of launch {k}")
+    assert sum(g[0].shape[0] for g in got) > 20   # episodes finished (games end from ~50 steps)

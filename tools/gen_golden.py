@@ -12,6 +12,8 @@ What is imported from /root/reference (read-only; nothing is copied):
   * environments/env_helper.py               (loaded by file path: execute_full_move_on_board_copy,
                                               generate_all_board_features, reward predicates)
   * agents/policy_network.py                 (loaded by file path: BackgammonPolicyNetwork)
+  * agents/trainer.py, environments/episode.py (loaded by file path: Trainer.update on 200
+                                              episodes; --only trainer, see main_trainer)
   * src/play/backgammon_256_standard_episode_2100000.pth (torch.load(weights_only=True))
 
 Two reference modules cannot be imported as-is because they need packages
@@ -692,10 +694,159 @@ def main_two_ply():
     gen_two_ply(net0, netc, positions, rng, t0)
 
 
+def _pack_words(b, mover):
+    """u8[52] board + the mover -> the record's packed words 0..6 (bgx/records.py:
+    point nibbles, then bar / borne-off nibbles and the mover at bit 16)."""
+    w = np.zeros(7, np.uint32)
+    for k in range(6):
+        for q in range(8):
+            w[k] |= np.uint32(int(b[8 * k + q]) << (4 * q))
+    w[6] = np.uint32(int(b[48]) | int(b[49]) << 4 | int(b[50]) << 8 | int(b[51]) << 12 | int(mover) << 16)
+    return w
+
+
+def _load_reference_trainer():
+    """src/agents/trainer.py loaded by file path. Its telemetry imports have no
+    package here: pynvml (GPU utilisation prints, trainer.py:3, 41, 55-56,
+    171-172) and S3Logger (tensorboardX / boto3 uploads, :6, 44-46, 187-230)
+    are replaced by no-op recorders -- the S3Logger stand-in keeps the
+    add_scalar(s) calls, which carry the update's metrics. Everything the
+    update computes (trainer.py:81-166) is the reference's own code."""
+    import types
+    nv = types.ModuleType("pynvml")
+    nv.nvmlDeviceGetHandleByIndex = lambda i: None
+    nv.nvmlDeviceGetUtilizationRates = lambda h: types.SimpleNamespace(gpu=0)
+    nv.nvmlDeviceGetMemoryInfo = lambda h: types.SimpleNamespace(used=0)
+    sys.modules["pynvml"] = nv
+
+    class S3Logger:
+        scalars = []
+
+        def __init__(self, *a, **k):
+            self.writer = types.SimpleNamespace(flush=lambda: None)
+
+        def add_scalar(self, tag, value, step):
+            S3Logger.scalars.append((tag, float(value), int(step)))
+
+        def add_scalars(self, tag, values, step):
+            S3Logger.scalars.append((tag, dict(values), int(step)))
+
+        def add_histogram(self, *a, **k):
+            pass
+
+    pkg = types.ModuleType("ref_agents")
+    pkg.__path__ = [os.path.join(REF, "src", "agents")]
+    sys.modules["ref_agents"] = pkg
+    lg = types.ModuleType("ref_agents.logger")
+    lg.S3Logger = S3Logger
+    sys.modules["ref_agents.logger"] = lg
+    sys.modules["ref_agents.policy_network"] = policy_network
+    spec = importlib.util.spec_from_file_location("ref_agents.trainer", os.path.join(REF, "src/agents/trainer.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ref_agents.trainer"] = mod
+    spec.loader.exec_module(mod)
+    return mod.Trainer, S3Logger
+
+
+def main_trainer(n_eps=200):
+    """tests/golden/trainer.npz: one reference Trainer.update (trainer.py:48-166)
+    of MIN_EPISODES_TO_TRAIN = 200 episodes on the seed-1 xavier network.
+
+    Inputs (synthetic, seeded): episode lengths 1..90 (a length-1 episode
+    included), self-play and random positions as the before-boards, the mover
+    alternating, shaping rewards 0 / 0.2 / 0.3 / 0.5 on the way and 1 / 2 / 2.5 on
+    terminal steps. Experience.observation = the reference encoder
+    (ImmutableBoard.get_board_features(mover), immutable_board.py:86-128),
+    reward a float32 tensor, as Episode.to_tensor leaves them (episode.py:30-46).
+    Stored as the engine's compact records (bgx/records.py) so the HIP trainer
+    takes them as is. Expected: the state_dict after the update and the logged
+    metrics (average loss, TD error, post-clip gradient norm, predicted value,
+    reward, episode length, win counts)."""
+    ep_mod = _load("ref_episode", "src/environments/episode.py")
+    Trainer, Log = _load_reference_trainer()
+    rng = np.random.default_rng(20261018)
+    pos = selfplay_positions(rng, 30)
+    for mode, cnt in (("general", 200), ("bar", 100), ("bearoff", 100), ("race", 50)):
+        pos += [rand_board(rng, mode) for _ in range(cnt)]
+    lens = rng.integers(2, 91, size=n_eps)
+    lens[7] = 1
+    shaping = np.array([0.0, 0.2, 0.3, 0.5], np.float32)
+    terminal = np.array([1.0, 2.0, 2.5], np.float32)
+    wins = {1.0: 1, 2.0: 2, 2.5: 3}
+    hdrs, recs, episodes = [], [], []
+    first = 0
+    for e in range(n_eps):
+        n = int(lens[e])
+        done_last = rng.random() < 0.8
+        ep = ep_mod.Episode()
+        mover0 = int(rng.integers(0, 2))
+        win = 0
+        for k in range(n):
+            b, _ = pos[int(rng.integers(0, len(pos)))]
+            mover = (mover0 + k) & 1
+            last = k == n - 1
+            r = float(rng.choice(terminal)) if (last and done_last) else float(shaping[rng.integers(0, 4)]
+                                                                                if rng.random() < 0.3 else 0.0)
+            if last and done_last:
+                win = wins[r]
+            obs = to_ib(b).get_board_features(Player(mover)).to(torch.float32)
+            ep.experiences.append(ep_mod.Experience(observation=obs, state_value=0.0,
+                                                    reward=torch.tensor(r, dtype=torch.float32),
+                                                    done=bool(last and done_last), next_observation=obs,
+                                                    next_state_value=0.0))
+            w = _pack_words(b, mover)
+            rec = np.zeros(12, np.uint32)
+            rec[:7] = w
+            rec[9] = np.float32(r).view(np.uint32)
+            rec[10] = np.uint32((1 << 11) | (min(k, 511) << 23))
+            rec[11] = np.uint32(1 | 2 << 3 | int(last and done_last) << 6 | mover << 9 | win << 10)
+            recs.append(rec)
+        ep.win_type = {0: None, 1: "regular", 2: "gammon", 3: "backgammon"}[win]
+        episodes.append(ep)
+        h = np.zeros(16, np.uint32)
+        h[0], h[1], h[2], h[3], h[4] = e, e, first, n, n
+        h[5] = win | ((mover0 + n - 1) & 1) << 8
+        hdrs.append(h)
+        first += n
+
+    class PM:
+        def __init__(self, sd):
+            self.sd = sd
+
+        def get_parameters(self):
+            return {k: v.clone() for k, v in self.sd.items()}
+
+        def set_parameters(self, sd):
+            self.sd = {k: v.detach().clone() for k, v in sd.items()}
+
+    torch.manual_seed(1)
+    sd0 = {k: v.clone() for k, v in policy_network.BackgammonPolicyNetwork().state_dict().items()}
+    pm = PM(sd0)
+    tr = Trainer(pm, device=torch.device("cpu"))
+    tr.update(episodes)
+    m = {t: v for t, v, _ in Log.scalars}
+    out = {"headers": np.stack(hdrs), "records": np.stack(recs)}
+    for k, v in sd0.items():
+        out["init_" + k.replace(".", "_")] = v.numpy()
+    for k, v in pm.sd.items():
+        out["after_" + k.replace(".", "_")] = v.numpy()
+    names = {"loss": "Loss/Training Loss", "td_error": "TD Error/Mean TD Error", "grad_norm": "Gradients/Gradient Norm",
+             "predicted_value": "Values/Average Predicted Value", "reward": "Rewards/Average Reward per Episode",
+             "episode_length": "Episode/Average Episode Length"}
+    for k, t in names.items():
+        out["metric_" + k] = np.float64(m[t])
+    wc = m["Wins"]
+    out["win_counts"] = np.array([wc["regular"], wc["gammon"], wc["backgammon"]], np.int64)
+    np.savez_compressed(os.path.join(OUT, "trainer.npz"), **out)
+    print(f"[gen] trainer: {n_eps} episodes, {first} records; loss {out['metric_loss']:.6g}", flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--only", "two_ply"]:
         main_two_ply()
     elif sys.argv[1:] == ["--only", "env"]:
         main_env()
+    elif sys.argv[1:] == ["--only", "trainer"]:
+        main_trainer()
     else:
         main()
