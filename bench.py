@@ -54,6 +54,7 @@ def load_weights():
 
 
 BACKEND = os.environ.get("BGX_DIST_BACKEND", "nccl")   # "gloo": rehearsal with ranks sharing GPUs
+FAIL_RANK = int(os.environ.get("BGX_BENCH_FAIL_RANK", "-1"))   # test hook: this rank raises mid-run
 
 
 def _coll_device():
@@ -125,6 +126,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
                  fused=not args.no_fused, balance=not args.no_balance)
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
+    harvested = [0, 0]   # this rank's own harvests (episodes, records), every run() of the engine
     hg = None
     if world > 1 and args.gather in ("host", "device"):
         from bgx import devgather, hostgather
@@ -151,6 +153,10 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
                 eng.harvest_fetch(t, wrap=False)   # the harvest ran on the device; nobody reads it here
                 return
             h = eng.harvest_fetch(t)
+            harvested[0] += h.n_episodes
+            harvested[1] += h.n_records
+            if FAIL_RANK == rank and seq[0] >= 1:   # test hook: this rank dies mid-run (after one batch)
+                raise RuntimeError(f"BGX_BENCH_FAIL_RANK: rank {rank} fails on purpose")
             if hg is not None:      # DMA engines into host shared memory / rank 0's GPU; no collective
                 seq[0] += 1
                 if rank == 0:
@@ -222,7 +228,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
         import torch.distributed as dist
         dist.barrier()
         hg.close()
-    return el, d, tm, d_tm, gathered
+    return el, d, tm, d_tm, gathered, harvested
 
 
 CPU_WARMUP_STEPS = 300   # BASELINE.md's CPU plan: a 300-step warm-up, then the timed window
@@ -482,7 +488,7 @@ def main():
 
     def leg(ply, k_top, lanes, steps, warmup, timing_steps, name, desync=None, seed=None):
         desync = args.desync_steps if desync is None else desync
-        el_, d_, tm_, dtm_, gathered_ = run_engine(args, world, rank, ply, k_top, lanes, steps, warmup,
+        el_, d_, tm_, dtm_, gathered_, harvested_ = run_engine(args, world, rank, ply, k_top, lanes, steps, warmup,
                                                    args.harvest_every, timing=timing_steps > 0,
                                                    timing_steps=timing_steps, desync=desync, seed=seed)
         el_ = max_over_ranks(el_, world)
@@ -499,6 +505,9 @@ def main():
                 "seed": args.seed if seed is None else seed}
         if world > 1:
             out_["gathered_episodes"], out_["gathered_records"] = gathered_
+            # what each rank harvested (all of the engine's runs, as the gather counts)
+            out_["harvested_episodes_per_rank"] = [int(x) for x in all_ranks(harvested_[0], world)]
+            out_["harvested_records_per_rank"] = [int(x) for x in all_ranks(harvested_[1], world)]
         if rank == 0:   # progress on stderr (the JSON line is stdout's only line)
             print(f"[bench] {name} lanes={lanes} seed={out_['seed']} steps={steps}: {out_['value'] / 1e6:.2f} M env "
                   f"steps/s, {out_['ms_per_step']:.4f} ms/step", file=sys.stderr, flush=True)
@@ -584,7 +593,9 @@ def main():
                                       if world == 1 else ""),
         }
         if world > 1:
-            line["gathered_episodes"], line["gathered_records"] = head["gathered_episodes"], head["gathered_records"]
+            for k in ("gathered_episodes", "gathered_records", "harvested_episodes_per_rank",
+                      "harvested_records_per_rank"):
+                line[k] = head[k]
         line.update(extra)
         print(json.dumps(line))
     if world > 1:

@@ -22,6 +22,7 @@ without touching host memory.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -160,13 +161,15 @@ class DeviceGather(HostGather):
         super().close()
 
 
-def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None) -> DeviceGather:
+def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None, timeout=None) -> DeviceGather:
     """Collective once (torch.distributed): the control segments as
     hostgather.setup, then dst's slots exported and opened by every peer."""
     import torch.distributed as dist
     obj = [make_tag() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
-    g = DeviceGather(rank, world, obj[0], slot_bytes, dst=dst, device=device)
+    if timeout is None:   # seconds a rank waits for a peer before it fails (BGX_GATHER_TIMEOUT)
+        timeout = float(os.environ.get("BGX_GATHER_TIMEOUT", "120"))
+    g = DeviceGather(rank, world, obj[0], slot_bytes, dst=dst, device=device, timeout=timeout)
     g.listen()
     dist.barrier()
     g.send_segment()

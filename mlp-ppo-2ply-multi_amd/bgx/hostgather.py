@@ -321,13 +321,15 @@ def make_tag() -> str:
     return f"{os.getpid()}_{secrets.token_hex(4)}"
 
 
-def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None) -> HostGather:
+def setup(rank: int, world: int, slot_bytes: int, dst: int = 0, device=None, timeout=None) -> HostGather:
     """Collective once (torch.distributed): agree on a tag, create the
     segments, hand their descriptors to dst. No collective afterwards."""
     import torch.distributed as dist
     obj = [make_tag() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
-    g = HostGather(rank, world, obj[0], slot_bytes, dst=dst, device=device)
+    if timeout is None:   # seconds a rank waits for a peer before it fails (BGX_GATHER_TIMEOUT)
+        timeout = float(os.environ.get("BGX_GATHER_TIMEOUT", "120"))
+    g = HostGather(rank, world, obj[0], slot_bytes, dst=dst, device=device, timeout=timeout)
     g.listen()
     dist.barrier()
     g.send_segment()

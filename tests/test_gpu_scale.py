@@ -180,3 +180,64 @@ def test_2ply_same_seed_same_records(weights_seed0, k_top, sample):
         runs.append(_by_episode(*_collect(e, 90 if k_top else 60, chunk=30)))
         e.close()
     _same_runs(*runs)
+
+
+def test_k4_8192_lanes_greedy_is_oracle_argmax(weights_seed0):
+    """2-ply K = 4 at the 8,192-lane shard (configs[4]'s per-GPU shape, the
+    bench's 2-ply leg), greedy, after >= 100 steps: >= 2,000 sampled decisions
+    equal the oracle's argmax of 1.0 * V - 0.9 * W over the top 4 by V
+    (two_ply.py:44-90, 153-193; fewer than 4 moves: the 1-ply argmax)."""
+    from bgx.episodes import decode_records
+    from test_gpu_replay import _two_ply_scores
+    e = _engine(weights_seed0, lanes=8192, seed=23, ply=2, k_top=4, greedy=True)
+    e.step(100)
+    e.harvest()
+    e.step(40)
+    h = e.harvest()
+    hdr = h.headers.cpu().numpy().view(np.uint32)
+    d = decode_records(hdr, h.records)
+    e.close()
+    m = d["action"].shape[0]
+    assert m > 10000
+    rng = np.random.default_rng(11)
+    ks = rng.choice(m, 2400, replace=False)
+
+    def one(k):
+        a = int(d["action"][k])
+        r = _two_ply_scores(weights_seed0, d["before"][k], int(d["mover"][k]), *d["dice"][k], 4)
+        if r[0] is None:
+            v = r[1]
+            return "1ply", v[a] >= v.max() - V_TOL, (a, float(v[a]), float(v.max()))
+        cand, score, v = r
+        if a not in set(cand.tolist()):   # only a V tie at the top-4 boundary moves a candidate in or out
+            return "tie", abs(v[a] - v[cand[-1]]) < V_TOL, (a, float(v[a]), float(v[cand[-1]]))
+        return "2ply", score[list(cand).index(a)] >= score.max() - 2 * V_TOL, (a, score.tolist())
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(one, ks))
+    for k, (kind, ok, info) in zip(ks, res):
+        assert ok, (int(k), kind, info)
+    assert sum(kind == "2ply" for kind, _, _ in res) >= 2000
+
+
+def test_k4_8192_lanes_sampling_transitions(weights_seed0):
+    """2-ply K = 4 sampling at 8,192 lanes: a seeded sample of whole episodes
+    holding >= 5,000 records replayed through the oracle transition by
+    transition (afterstate, V(s) / V(a), rewards, observations; the chosen
+    move is one of the legal ones)."""
+    import torch
+    from bgx.episodes import decode_records
+    e = _engine(weights_seed0, lanes=8192, seed=29, ply=2, k_top=4)
+    e.step(150)
+    h = e.harvest()
+    hdr = h.headers.cpu().numpy().view(np.uint32)
+    rec = h.records.cpu().numpy().view(np.uint32)
+    e.close()
+    assert _check_headers([(hdr, rec)], 8192) > 1000
+    rng = np.random.default_rng(5)
+    order = rng.permutation(hdr.shape[0])
+    lens = hdr[order, 3].astype(np.int64)
+    take = order[:int(np.searchsorted(np.cumsum(lens), 5000)) + 1]
+    sub_h, sub_r = _subset(hdr, rec, np.sort(take))
+    d = decode_records(sub_h, torch.from_numpy(sub_r.view(np.int32)).cuda())
+    assert _check_transitions(weights_seed0, [sub_h], [d], 2) >= 5000
