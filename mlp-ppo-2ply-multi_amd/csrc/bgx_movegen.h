@@ -28,6 +28,14 @@ static __device__ unsigned long long bgx_stamp_acc[256 * 32];
 #define STAMP_COUNT(k)
 #endif
 
+// Development builds (-DBGX_DBL_GUARD=1, tools/runs/dbl_guard.sh): every global
+// write of the movegen kernels, and the reply launch's input reads, check their
+// index and set an error bit (0x100..0x8000, reported as "overflow flags" by the
+// ABI) instead of touching memory out of range.
+#ifndef BGX_DBL_GUARD
+#define BGX_DBL_GUARD 0
+#endif
+
 constexpr unsigned long long EMPTY64 = ~0ull;
 constexpr uint32_t KEY_EMPTY4 = 0xFFFFFu;   // four empty 5-bit fields
 constexpr uint32_t KEYMASK = 0xFFFFFu;
@@ -349,6 +357,14 @@ BGX_DEV JobIn make_job(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint3
 constexpr uint32_t SKIP_ROW = 0xFFFFFFFFu;
 struct RawJob { uint32_t v; };
 
+BGX_DEV int job_count(const MovegenArgs& a) {
+    int n = a.n_jobs;
+    if (a.n_jobs_dev) n += (int)(*a.n_jobs_dev) * a.jobs_per_dev_unit;
+    if (a.n_jobs_max > 0 && n > a.n_jobs_max) n = a.n_jobs_max;
+    return n;
+}
+
+
 BGX_DEV RawJob fetch_raw(const MovegenArgs& a, int j) {
     const int l = lane_id();
     uint32_t v = 0u;
@@ -358,6 +374,10 @@ BGX_DEV RawJob fetch_raw(const MovegenArgs& a, int j) {
         int src = j;
         if (a.in_mode == IN_TWOPLY) {
             const int row = j / 21;
+            if (BGX_DBL_GUARD && (j < 0 || j >= job_count(a))) {
+                if (l == 0) atomicOr(a.err_flags, 0x8000u);
+                return {0u};
+            }
             src = a.in_rows ? a.in_rows[row] : a.in_row_base + row;
         }
         if (l < 8) v = src < 0 ? (l == 7 ? SKIP_ROW : 0u) : a.in_packed[(size_t)src * 8 + l];
@@ -442,18 +462,15 @@ BGX_DEV void emit_one(const MovegenArgs& a, int j, const Root& R, const Node& n,
         if (k >= a.cap) return;
         row = (size_t)j * a.cap + k;
     } else {
+        if (BGX_DBL_GUARD && (base < 0 || k < 0 || base + k >= a.flat_cap)) {
+            atomicOr(a.err_flags, 0x2000u);
+            return;
+        }
         row = (size_t)base + k;
     }
     uint4* dst = (uint4*)(a.out_packed + row * 8);
     dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
     dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
-
-BGX_DEV int job_count(const MovegenArgs& a) {
-    int n = a.n_jobs;
-    if (a.n_jobs_dev) n += (int)(*a.n_jobs_dev) * a.jobs_per_dev_unit;
-    if (a.n_jobs_max > 0 && n > a.n_jobs_max) n = a.n_jobs_max;
-    return n;
 }
 
 // Per-wave output reservation for OUT_PACKED_FLAT: one global atomic per
@@ -514,8 +531,12 @@ BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
             }
         }
         if (lane_id() == 0) {
-            a.job_off[j] = base < 0 ? 0 : base;
-            a.job_cnt[j] = base < 0 ? 0 : n;
+            if (BGX_DBL_GUARD && (j < 0 || j >= job_count(a))) {
+                atomicOr(a.err_flags, 0x1000u);
+            } else {
+                a.job_off[j] = base < 0 ? 0 : base;
+                a.job_cnt[j] = base < 0 ? 0 : n;
+            }
         }
     } else if (lane_id() == 0) {
         a.out_count[j] = n;
@@ -1054,9 +1075,6 @@ BGX_DEV int path_doubles_emit(const MovegenArgs& a, int j, const JobIn& in, cons
 // per-roll jobs: all six when the root is not in path mode, the unfinished
 // ones when a level outgrows the slice's list.
 constexpr uint32_t DIE_SHIFT = 20;   // list entry: path | die << 20 | PATHF | FLAG1
-#ifndef BGX_DBL_GUARD
-#define BGX_DBL_GUARD 0   // development builds: index checks that flag (err bits 0x100..) instead of writing
-#endif
 // index in the 21 DICE_ROLLS of the q-th non-doubles roll (the doubles sit at 0, 6, 11, 15, 18, 20)
 BGX_DEV int nd_roll_q21(int q) { return q + 1 + (q >= 5) + (q >= 9) + (q >= 12) + (q >= 14); }
 BGX_DEV int dbl_q21(int d) { return (d - 1) * 7 - ((d - 1) * d) / 2; }   // (d, d), d = 1..6
@@ -1890,6 +1908,10 @@ BGX_DEV Mem lds_mem(unsigned long long* smem) {
 }
 
 BGX_DEV void push_ovf(const MovegenArgs& a, int j) {
+    if (BGX_DBL_GUARD && (j < 0 || j >= job_count(a))) {
+        atomicOr(a.err_flags, 0x4000u);
+        return;
+    }
     const unsigned slot = atomicAdd(a.ovf_count, 1u);
     if ((int)slot < a.ovf_cap) a.ovf_list[slot] = j;
     else atomicOr(a.err_flags, BGX_ERRF_OVF_LIST);

@@ -312,8 +312,12 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                 const int pre = wave_incl_scan(rc) - rc;
                 if (l < ND_ROLLS) {
                     const int j = j0 + nd_roll_q21(l);
-                    a.job_off[j] = base < 0 ? 0 : base + pre;
-                    a.job_cnt[j] = base < 0 ? 0 : rc;
+                    if (BGX_DBL_GUARD && (j >= n_jobs || (base >= 0 && base + pre + rc > a.flat_cap))) {
+                        atomicOr(a.err_flags, 0x1000u);
+                    } else {
+                        a.job_off[j] = base < 0 ? 0 : base + pre;
+                        a.job_cnt[j] = base < 0 ? 0 : rc;
+                    }
                 }
                 if (base >= 0) {
                     for (int i = l; i < n; i += 64) {

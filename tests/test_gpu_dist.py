@@ -191,15 +191,18 @@ def test_host_gather_world2_real_harvests(weights_seed0, mode):
         return {(int(r[0]), int(r[1])): (r.copy(), rec[offs[i]:offs[i + 1]]) for i, r in enumerate(hdr)}
 
     assert len(got) == len(want)
+    total = 0
     for parts, (wh, wr) in zip(got, want):
         merged = {}
         for hh, rr in parts:
             merged.update(by_episode(hh, rr))
         ref = by_episode(wh, wr)
-        assert merged.keys() == ref.keys() and len(ref) > (0 if chunks else 20)
+        assert merged.keys() == ref.keys()
+        total += len(ref)
         for key in ref:
             np.testing.assert_array_equal(merged[key][0], ref[key][0], err_msg=str(key))
             np.testing.assert_array_equal(merged[key][1], ref[key][1], err_msg=str(key))
+    assert total > 40   # games end from ~50 steps: the later batches hold the episodes
 
 
 def _nccl_rank(rank, world, port, L, steps, out):
