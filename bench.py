@@ -149,6 +149,10 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
 
         def consume(t):
             nonlocal inflight
+            # the previous hand-off first: the loop's last consume and the final one
+            # come back to back, and a Pending replaced without its wait() would
+            # never publish its batch (rank 0 would read that slot's stale counts)
+            settle()
             if world == 1:
                 eng.harvest_fetch(t, wrap=False)   # the harvest ran on the device; nobody reads it here
                 return

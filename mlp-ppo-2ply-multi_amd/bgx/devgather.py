@@ -100,6 +100,8 @@ class DeviceGather(HostGather):
         n_eps, n_recs = h.n_episodes, h.n_records
         if self.broken:
             raise RuntimeError("DeviceGather: an earlier DMA copy did not finish; its slot is still owned by it")
+        if self.open_batch is not None and not self.open_batch.done:
+            raise RuntimeError(f"DeviceGather: batch {self.open_batch.seq} was not waited for before the next publish")
         need = n_eps * EP_BYTES + n_recs * REC_BYTES
         if need > self.slot_bytes:   # before the batch number moves: dst still waits for the same batch
             raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")

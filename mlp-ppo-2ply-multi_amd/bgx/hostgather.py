@@ -80,6 +80,8 @@ class Pending:
         self.g, self.seq, self.n_eps, self.n_recs, self.slot, self.event = gather, seq, n_eps, n_recs, slot, event
         self.dma = dma
         self.keep = keep
+        self.done = False
+        gather.open_batch = self
 
     def wait(self):
         if self.event is not None:
@@ -102,6 +104,7 @@ class Pending:
         c = self.g.ctrl[self.g.rank]
         c[1 + 2 * self.slot], c[2 + 2 * self.slot] = self.n_eps, self.n_recs
         c[0] = self.seq            # publishes (aligned 8-byte store after the counts)
+        self.done = True
         return self.seq
 
 
@@ -142,6 +145,7 @@ class HostGather:
         self.timeout = timeout
         self.device = device
         self.seq = 0
+        self.open_batch = None   # the last Pending: a batch is published by its wait(), before the next one
         self.broken = False   # a DMA copy of this gather timed out (Pending.wait): no further batches
         self._mine = _Segment(self._name(rank), size=HDR + 2 * self.slot_bytes)
         self.shm = {rank: self._mine}
@@ -222,6 +226,10 @@ class HostGather:
         n_eps, n_recs = h.n_episodes, h.n_records
         if self.broken:
             raise RuntimeError("HostGather: an earlier DMA copy did not finish; its slot is still owned by it")
+        if self.open_batch is not None and not self.open_batch.done:
+            # publishing c[0] = seq + 1 first would make dst read batch seq's slot
+            # with the counts of the batch before it
+            raise RuntimeError(f"HostGather: batch {self.open_batch.seq} was not waited for before the next publish")
         need = n_eps * EP_BYTES + n_recs * REC_BYTES
         if need > self.slot_bytes:   # before the batch number moves: dst still waits for the same batch
             raise ValueError(f"harvest of {need} bytes > slot of {self.slot_bytes} (slot_bytes_for)")

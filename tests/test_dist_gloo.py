@@ -221,3 +221,27 @@ def test_host_gather_oversized_harvest_keeps_batch_numbers():
         assert p.wait() == 1 and int(g.ctrl[1][0]) == 1
     finally:
         g.close()
+
+
+def test_host_gather_refuses_publish_before_wait():
+    """A batch is published by its Pending.wait(): a second publish before it
+    would move the batch number past a batch whose counts were never written,
+    and dst would read that slot with the counts of the batch before it (the
+    round-5 fan-in rehearsal lost 1,315 of 7,657 episodes that way in
+    bench.py). The gather refuses it."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    from bgx import hostgather
+    from bgx.engine import Harvest
+    g = hostgather.HostGather(1, 2, hostgather.make_tag(), slot_bytes=4096)
+    try:
+        h = Harvest(torch.ones((1, 16), dtype=torch.int32), torch.ones((2, 12), dtype=torch.int32))
+        p = g.publish(h)
+        with pytest.raises(RuntimeError, match="not waited"):
+            g.publish(h)
+        assert p.wait() == 1 and int(g.ctrl[1][0]) == 1
+        g.ctrl[1][5] = 1
+        assert g.publish(h).wait() == 2
+    finally:
+        g.close()
