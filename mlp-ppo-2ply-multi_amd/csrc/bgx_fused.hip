@@ -29,6 +29,9 @@
 #include "bgx_mlp.h"
 #include "bgx_movegen.h"
 
+#ifndef BGX_HALF_TICKETS
+#define BGX_HALF_TICKETS 1   // balanced launches: half-lane tickets in the last round (0: whole-group tickets; A/B)
+#endif
 #ifndef BGX_FUSED_LEAF
 #define BGX_FUSED_LEAF 0   // A/B builds: 1 = tier-1 path doubles stream their leaves (run_job<LEAF>)
 #endif
@@ -98,6 +101,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     for (int i = t; i < 64; i += NT) T.tdone[i] = 0u;
     for (int i = t; i < FL; i += NT) T.chosen[i] = T.claim[i] = 0u;
     unsigned qtag = 0u;   // this workgroup's step counter (tags the flags; never 0 on a live step)
+    int half_b = 0;       // thread 0: the half a half-lane ticket steps next (ticket)
     // split-fp16 W fragments, loaded once, global -> LDS by LDS-DMA (every load
     // of a wave in flight at once; the prologue's lane loads overlap them)
     uint4* wl = (uint4*)(lds + F_W);
@@ -180,11 +184,30 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         // budget (thread 0 takes step s + 1's ticket after step s's queue, which
         // expanded the next positions whatever the ticket says: a refused ticket
         // ends the launch with them ready for the next one)
+        // A ticket is the step's lane range, lo | hi << 8 (0: stop). In the
+        // launch's last round (less than one full step of every workgroup left in
+        // the budget) a balanced workgroup steps half its lanes at a time, the two
+        // halves in turn: a half step is ~0.6 of a full one, so the workgroups'
+        // ends, spread over the step that each was in when the budget ran out,
+        // lie closer together. Each lane's game is its own (dice and uniforms are
+        // keyed by lane and its counter), so which lanes step when changes nothing
+        // but how far each lane has got at a harvest.
         auto ticket = [&](int s) -> int {
-            if (f.budget <= 0) return s < f.n_steps;
+            const int full = nlive << 8;
+            if (f.budget <= 0) return s < f.n_steps ? full : 0;
             if (s >= f.n_cap) return 0;
-            const unsigned long long old = atomicAdd(f.budget_ctr, (unsigned long long)nlive);
-            return old < (unsigned long long)f.budget;
+            int lo = 0, hi = nlive;
+            if (BGX_HALF_TICKETS && nlive >= 2) {
+                const long long left =
+                    f.budget - (long long)__hip_atomic_load(f.budget_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (left < (long long)gridDim.x * (long long)nlive) {
+                    half_b ^= 1;
+                    lo = half_b ? nlive >> 1 : 0;
+                    hi = half_b ? nlive : nlive >> 1;
+                }
+            }
+            const unsigned long long old = atomicAdd(f.budget_ctr, (unsigned long long)(hi - lo));
+            return old < (unsigned long long)f.budget ? lo | (hi << 8) : 0;
         };
         // bounded wait for an LDS flag
         auto wait_flag = [&](const unsigned* fl) {
@@ -206,12 +229,16 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         // inlined once each).
         for (int step = -1; step < n_iter; ++step) {
             int nr = 0;
-            if (step >= 0 && !T.go[step & 1]) break;
+            // this step's lanes [lo, hi) (step -1, the first step's tier-1 jobs: all)
+            const int gv = step >= 0 ? T.go[step & 1] : nlive << 8;
+            if (!gv) break;
+            const int lo = gv & 255, hi = gv >> 8;
+            const auto act = [&](int v) { return v >= lo && v < hi; };
             if (prof && t == 0) tc = wall_clock64();
             if (step >= 0) {
-                n_steps += (unsigned long long)nlive;
+                n_steps += (unsigned long long)(hi - lo);
                 // ---- 1b. jobs that outgrew their slice: the workgroup, one at a time (rare)
-                const int cnt_l = l < nlive ? T.cnt[l] : 0;   // lane q < FL holds lane q's count
+                const int cnt_l = act(l) ? T.cnt[l] : 0;   // lane q < FL holds lane q's count
                 uint32_t ovf = (uint32_t)ballot(l < FL && cnt_l < 0);
                 while (ovf) {
                     const int v = __ffs(ovf) - 1;
@@ -265,7 +292,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 }
                 // ---- 2. row prefix (lanes that pass evaluate nothing), every wave
                 // computes it (identical values)
-                const int c = l < nlive ? T.cnt[l] : 0;
+                const int c = act(l) ? T.cnt[l] : 0;   // lanes outside this step's range: no rows
                 const int rows = l < FL && c > 0 ? 1 + (c < f.cap ? c : f.cap) : 0;
                 const int incl = wave_incl_scan(rows);
                 if (l <= FL) T.pre[l] = incl - rows;
@@ -275,7 +302,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                 tick(1);
             }
             const int n_tiles = (nr + 31) >> 5;
-            const int np = step >= 0 ? (nlive + 1) >> 1 : 0;   // choice items: lane pairs
+            const int np = step >= 0 ? (hi - lo + 1) >> 1 : 0;   // choice items: lane pairs
             if (t == 0) {
                 T.qn[0] = NW;
                 T.qn[1] = NW;
@@ -287,10 +314,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             // step s + 1's tier-1 jobs (every step: the last one's results are
             // the next launch's first; at step -1, unless the previous launch
             // left them)
-            const int nj = step >= 0 || !f.t1_ready ? nlive : 0;
+            const int nj = step >= 0 || !f.t1_ready ? hi - lo : 0;
             // the next step's jobs, doubles first, when nothing runs beside them
-            const bool dbl = l < nlive && T.st[l].d0 == T.st[l].d1;
-            const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(l < nlive && !dbl);
+            const bool dbl = act(l) && T.st[l].d0 == T.st[l].d1;
+            const uint32_t dmask = (uint32_t)ballot(dbl), omask = (uint32_t)ballot(act(l) && !dbl);
             const int nd = __popc(dmask);
             // row r of the workgroup -> its lane: the last v with pre[v] <= r
             auto lane_of = [&](int r) -> int {
@@ -357,16 +384,16 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                         // ---- 4. action choice + env step of two lanes, one per half-wave
                         const int p = it - qt;
                         if (pipelined) {
-                            const int va = 2 * p, vb = 2 * p + 2 < nlive ? 2 * p + 2 : nlive;
+                            const int va = lo + 2 * p, vb = lo + 2 * p + 2 < hi ? lo + 2 * p + 2 : hi;
                             const int r0 = T.pre[va], r1 = T.pre[vb];   // the pair's rows [r0, r1)
                             if (r1 > r0) {
                                 for (int tt = r0 >> 5; tt <= (r1 - 1) >> 5; ++tt) wait_flag(&T.tdone[tt]);
                                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                             }
                         }
-                        const int v = 2 * p + (l >> 5);
+                        const int v = lo + 2 * p + (l >> 5);
                         const bool lead = (l & 31) == 0;
-                        if (v < nlive) {
+                        if (v < hi) {
                             const int i = g * FL + v;
                             const unsigned long long s1 = prof ? wall_clock64() : 0ull;
                             LaneState sr = T.st[v];
@@ -416,7 +443,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             if (prof) tw[3] += wall_clock64() - s1;
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        if (lead && v < nlive)
+                        if (lead && v < hi)
                             __hip_atomic_store(&T.chosen[v], qtag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     } else {
                         // ---- 1. a tier-1 job of the next step in this wave's slice:
@@ -431,7 +458,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
                             v = -1;
                             for (unsigned spin = 0; v < 0; ++spin) {
                                 const bool ready =
-                                    l < nlive &&
+                                    act(l) &&
                                     __hip_atomic_load(&T.chosen[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == qtag &&
                                     __hip_atomic_load(&T.claim[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != qtag;
                                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

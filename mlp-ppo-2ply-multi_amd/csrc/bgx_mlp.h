@@ -5,6 +5,15 @@
 #include "bgx_device.h"
 #include "bgx_kernels.h"
 
+#ifndef BGX_TILE_PF
+#define BGX_TILE_PF 1      // > 0: mlp_tile4 reads its A fragments this many MFMA pairs ahead (0: the compiler's schedule; A/B)
+#endif
+#ifndef BGX_TILE_PRIO
+#define BGX_TILE_PRIO 1    // mlp_tile4 issues its MFMA chain at this wave priority (s_setprio; 0: none; A/B)
+#endif
+#ifndef BGX_TILE_PRIO_EPI
+#define BGX_TILE_PRIO_EPI 0   // 1: the priority holds through the epilogue (exp / rcp) too (A/B)
+#endif
 #ifndef BGX_TILE_NOSKIP
 #define BGX_TILE_NOSKIP 1   // 1: mlp_tile4 runs every k-step (straight-line code); 0: zero k-steps skipped (A/B builds)
 #endif
@@ -212,6 +221,39 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
     for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[m][r] = 0.0f;
+#if BGX_TILE_PF
+    // Software-pipelined fragment reads: the 52 (k-step, m-tile) pairs of A
+    // fragments (hi, lo) run through a ring of BGX_TILE_PF + 1 register pairs,
+    // read BGX_TILE_PF pairs ahead of their MFMAs, and the next k-step's feature
+    // fragment one m-tile round ahead. Left to itself the compiler issued each
+    // pair's two ds_read_b128 right before its MFMAs and waited for them there
+    // (lgkmcnt(1) / (0) before every MFMA), so each MFMA paid the LDS latency;
+    // the sched_barrier keeps the early reads in front. Same MFMAs in the same
+    // order on each accumulator: same bits.
+    constexpr int NP = 4 * KSTEPS, D = BGX_TILE_PF, NR = D + 1;
+    v4u ra[NR], rl[NR];
+    half8 rb[2];
+    auto ld = [&](int i) {
+        const int s = i >> 2, m = i & 3;
+        ra[i % NR] = wfh[(m * KSTEPS + s) * 64];
+        rl[i % NR] = wfl[(m * KSTEPS + s) * 64];
+    };
+    rb[0] = feat_frag(bx, by, 0, h, lut, fs);
+#pragma unroll
+    for (int i = 0; i < D; ++i) ld(i);
+    if (BGX_TILE_PRIO) __builtin_amdgcn_s_setprio(BGX_TILE_PRIO);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int s = i >> 2, m = i & 3;
+        if (i + D < NP) ld(i + D);
+        if (m == 0 && s + 1 < KSTEPS) rb[(s + 1) & 1] = feat_frag(bx, by, s + 1, h, lut, fs);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ra[i % NR]), rb[s & 1], acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, rl[i % NR]), rb[s & 1], acc[m], 0, 0, 0);
+    }
+    if (BGX_TILE_PRIO && !BGX_TILE_PRIO_EPI) __builtin_amdgcn_s_setprio(0);
+    (void)kmask;
+#else
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
         if (BGX_TILE_NOSKIP || (kmask & (1u << s))) {
@@ -225,6 +267,7 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
             }
         }
     }
+#endif
     if (STAMP) *stamp = wall_clock64();   // development (BGX_FUSED_PROF): the MFMA chain issued
     float v = 0.0f;
 #pragma unroll
@@ -244,6 +287,9 @@ BGX_DEV float mlp_tile4(const uint4* wf, const uint4* lut, const float* w2s, flo
         }
         v = m == 0 ? p : v + p;
     }
+#if BGX_TILE_PF
+    if (BGX_TILE_PRIO && BGX_TILE_PRIO_EPI) __builtin_amdgcn_s_setprio(0);
+#endif
     return v + __shfl_xor(v, 32, 64);
 }
 
