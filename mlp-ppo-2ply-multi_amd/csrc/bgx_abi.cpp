@@ -82,6 +82,8 @@ static int net_upload(bgx_net* n, const float* W1, const float* b1, const float*
     return BGX_OK;
 }
 
+constexpr int PROF_W = 128;   // u64 words per workgroup slot of the fused development report (bgx_fused.hip PROF_STRIDE)
+
 struct bgx_engine {
     int device = 0;
     bgx_config cfg{};
@@ -957,11 +959,11 @@ int bgx_engine_destroy(bgx_engine* e) {
         hipSetDevice(e->device);
         hipDeviceSynchronize();
         if (e->fprof) {   // development report (BGX_FUSED_PROF): per workgroup-step averages, wall clock 100 MHz
-            std::vector<unsigned long long> p((size_t)1024 * 32);
+            std::vector<unsigned long long> p((size_t)1024 * PROF_W);
             if (hipMemcpy(p.data(), e->fprof, p.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
                 double s[32] = {0};
                 for (int b = 0; b < 1024; ++b)
-                    for (int k = 0; k < 23; ++k) s[k] += (double)p[(size_t)b * 32 + k];
+                    for (int k = 0; k < 23; ++k) s[k] += (double)p[(size_t)b * PROF_W + k];
                 const double n = s[5] > 0 ? s[5] : 1;
                 const double nws = s[18] > 0 ? s[18] : 1;   // wave-steps
                 // (the pipelined kernel: each step is tier 2 + the row prefix, then one item
@@ -974,19 +976,33 @@ int bgx_engine_destroy(bgx_engine* e) {
                 {
                     double c[3] = {0, 0, 0};
                     for (int b = 0; b < 1024; ++b)
-                        for (int k = 0; k < 3; ++k) c[k] += (double)p[(size_t)b * 32 + 29 + k];
+                        for (int k = 0; k < 3; ++k) c[k] += (double)p[(size_t)b * PROF_W + 29 + k];
                     fprintf(stderr, "[bgx fused prof] choice per wave-step: state + Philox refill %.2f, pick %.2f, "
                             "env step %.2f us\n", c[0] / nws / 100, c[1] / nws / 100, c[2] / nws / 100);
                 }
                 {
                     double c[3] = {0, 0, 0};
                     for (int b = 0; b < 1024; ++b) {
-                        c[0] += (double)p[(size_t)b * 32 + 6];
-                        c[1] += (double)p[(size_t)b * 32 + 22];
-                        c[2] += (double)p[(size_t)b * 32 + 23];
+                        c[0] += (double)p[(size_t)b * PROF_W + 6];
+                        c[1] += (double)p[(size_t)b * PROF_W + 22];
+                        c[2] += (double)p[(size_t)b * PROF_W + 23];
                     }
                     fprintf(stderr, "[bgx fused prof] MLP tiles per workgroup step: rows + k mask %.2f, MFMA chain issue %.2f, "
                             "drain + epilogue %.2f wave-us\n", c[0] / n / 100, c[1] / n / 100, c[2] / n / 100);
+                }
+                {   // step durations by index within a launch (every launch, every workgroup)
+                    double st[24] = {0}, cn[24] = {0}, late = 0, nlate = 0;
+                    for (int b = 0; b < 1024; ++b) {
+                        for (int k = 0; k < 24; ++k) {
+                            st[k] += (double)p[(size_t)b * PROF_W + 32 + k];
+                            cn[k] += (double)p[(size_t)b * PROF_W + 64 + k];
+                        }
+                        late += (double)p[(size_t)b * PROF_W + 56];
+                        nlate += (double)p[(size_t)b * PROF_W + 57];
+                    }
+                    fprintf(stderr, "[bgx fused prof] step us by index in the launch (workgroup-steps):");
+                    for (int k = 0; k < 24; ++k) fprintf(stderr, " %.2f (%.0f)", cn[k] > 0 ? st[k] / cn[k] / 100 : 0.0, cn[k]);
+                    fprintf(stderr, "; later steps %.2f (%.0f)\n", nlate > 0 ? late / nlate / 100 : 0.0, nlate);
                 }
                 fprintf(stderr, "[bgx fused prof] tier-2 jobs %.0f (%.0f reached tier 3), %.1f us each\n", s[12], s[13],
                         s[11] / (s[12] > 0 ? s[12] : 1) / 100);
@@ -997,7 +1013,7 @@ int bgx_engine_destroy(bgx_engine* e) {
                 std::vector<std::pair<double, int>> dur;
                 unsigned long long b_min = ~0ull, b_max = 0, e_max = 0;
                 for (int b = 0; b < 1024; ++b) {
-                    const unsigned long long* q = &p[(size_t)b * 32];
+                    const unsigned long long* q = &p[(size_t)b * PROF_W];
                     if (q[25] <= q[24]) continue;
                     dur.push_back({(double)(q[25] - q[24]) / 100.0, b});
                     b_min = q[24] < b_min ? q[24] : b_min;
@@ -1010,7 +1026,7 @@ int bgx_engine_destroy(bgx_engine* e) {
                     if (FILE* fp = fopen(path, "w")) {
                         fprintf(fp, "wg,begin,end,loop0,loop1,rows,tier2,lane_steps\n");
                         for (int b = 0; b < 1024; ++b) {
-                            const unsigned long long* q = &p[(size_t)b * 32];
+                            const unsigned long long* q = &p[(size_t)b * PROF_W];
                             if (q[25] <= q[24]) continue;
                             fprintf(fp, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", b, q[24], q[25], q[19], q[20], q[26],
                                     q[27], q[28]);
@@ -1457,8 +1473,8 @@ static int enqueue_fused(bgx_engine* e, int n_steps, hipStream_t s) {
     }
     if (e->prof_enabled) {
         if (!e->fprof) {
-            if (dalloc(&e->fprof, (size_t)1024 * 32)) return BGX_E_HIP;
-            HIP_TRY(hipMemset(e->fprof, 0, (size_t)1024 * 32 * 8));
+            if (dalloc(&e->fprof, (size_t)1024 * PROF_W)) return BGX_E_HIP;
+            HIP_TRY(hipMemset(e->fprof, 0, (size_t)1024 * PROF_W * 8));
         }
         f.prof = e->fprof;
     }

@@ -30,13 +30,15 @@
 #include "bgx_movegen.h"
 
 #ifndef BGX_HALF_TICKETS
-#define BGX_HALF_TICKETS 1   // balanced launches: half-lane tickets in the last round (0: whole-group tickets; A/B)
+#define BGX_HALF_TICKETS 0   // 1: half-lane tickets in a balanced launch's last round (measured slower: DESIGN.md section 9; A/B)
 #endif
 #ifndef BGX_FUSED_LEAF
 #define BGX_FUSED_LEAF 0   // A/B builds: 1 = tier-1 path doubles stream their leaves (run_job<LEAF>)
 #endif
 
 namespace bgx {
+
+constexpr int PROF_STRIDE = 128;   // u64 words per workgroup slot of the development report (f.prof)
 
 // FL = game lanes per workgroup and NW = waves per workgroup: 16 lanes on 8
 // waves (2 per SIMD, 256 registers) when fewer lanes than 32 x CUs, else 32
@@ -127,6 +129,10 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
     const unsigned long long wg_begin = PROF ? wall_clock64() : 0ull;   // this launch's span (f.prof)
     const unsigned long long cyc_begin = PROF ? __builtin_amdgcn_s_memtime() : 0ull;   // shader clock (f.prof)
     unsigned long long t_loop0 = 0, t_loop1 = 0;   // first step's start, last step's end (f.prof)
+    // step durations by index within the launch (f.prof): steps 0..23 go to
+    // P[32 + k] (their count to P[64 + k]) as they end, later ones are summed here
+    unsigned long long t_step = 0, late_sum = 0, late_n = 0;
+    int step_idx = 0;
     // development timers (f.prof): phase sums on thread 0, per-wave sums on lane 0
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tc = 0, tw[4] = {0, 0, 0, 0}, t2c = 0, t3n = 0;
     unsigned long long tjd[4] = {0, 0, 0, 0};   // tier-1 job clocks / counts: doubles, non-doubles
@@ -522,6 +528,18 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             __syncthreads();   // step s's lanes are stepped and step s + 1's jobs are done
             tick(4);
             if (prof && t == 0 && step >= 0) ph[5] += 1;
+            if (prof && t == 0) {
+                const unsigned long long c = wall_clock64();
+                if (step >= 0) {
+                    if (step_idx < 24) {
+                        atomicAdd(f.prof + (size_t)blockIdx.x * PROF_STRIDE + 32 + step_idx, c - t_step);
+                        atomicAdd(f.prof + (size_t)blockIdx.x * PROF_STRIDE + 64 + step_idx, 1ull);
+                    }
+                    else { late_sum += c - t_step; ++late_n; }
+                    ++step_idx;
+                }
+                t_step = c;
+            }
         }
         if (prof && t == 0) t_loop1 = wall_clock64();
         for (int v = t; v < nlive; v += NT) {
@@ -617,7 +635,7 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
         __syncthreads();
     }
     if (prof) {
-        unsigned long long* P = f.prof + (size_t)blockIdx.x * 32;
+        unsigned long long* P = f.prof + (size_t)blockIdx.x * PROF_STRIDE;
         if (t == 0) {
             // the last launch's begin / end clocks, rows and tier-2 jobs of this
             // workgroup (overwritten per launch: the spread of the workgroups'
@@ -635,6 +653,8 @@ __global__ __launch_bounds__(64 * FCfg<FL>::NW, FCfg<FL>::WPE) void fused_step_k
             atomicAdd(P + 12, n_fb);
             atomicAdd(P + 13, t3n);
             atomicAdd(P + 18, (unsigned long long)NW * ph[5]);   // wave-steps
+            atomicAdd(P + 56, late_sum);
+            atomicAdd(P + 57, late_n);
         }
         if (l == 0) {
             for (int k = 0; k < 4; ++k) atomicAdd(P + 7 + k, tw[k]);

@@ -135,13 +135,15 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
 // items spread. Same records, offsets and counts per job as the pool kernel
 // (job order within a row's block is the DICE_ROLLS order); overflowing
 // per-roll jobs go to tier 2 as before.
-#ifndef BGX_DBL_BM
-#define BGX_DBL_BM 0   // 1: a row's six doubles rolls in one item (board_dbl_emit); 0: one item per roll
-#endif
-constexpr int REPLY_GROUPS = BGX_DBL_BM ? 2 : 7;
+// DBL (the launch picks it, bgx_launch_movegen): a row's six doubles rolls in
+// one item (board_dbl_emit), groups 0..1; otherwise one item per doubles roll,
+// groups 0..6.
+template <bool DBL> constexpr int reply_groups() { return DBL ? 2 : 7; }
 constexpr int REPLY_SUBQ = 1024;   // sub-queue entries per workgroup (4 KB of LDS: 2 x 68 KB per CU)
+template <bool DBL>
 __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_reply_kernel(
     MovegenArgs a0) {
+    constexpr int REPLY_GROUPS = reply_groups<DBL>();
     MovegenArgs a = a0;
     a.in_mode = IN_TWOPLY;
     a.out_mode = OUT_PACKED_FLAT;
@@ -171,9 +173,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     // one wave (at ~13 us per job that wave ends ~190 us after the others)
     __shared__ int subq[REPLY_SUBQ];
     __shared__ int sub_res, sub_head, items_done;
-#if BGX_DBL_BM
-    __shared__ uint32_t dcnt[PW][8];   // board_dbl_emit's per-die child counts, per wave
-#endif
+    __shared__ uint32_t dcnt[DBL ? PW : 1][8];   // board_dbl_emit's per-die child counts, per wave
     for (int i = (int)threadIdx.x; i < REPLY_SUBQ; i += 64 * PW) subq[i] = 0;
     if (threadIdx.x == 0) {
         next_job = PW;
@@ -195,7 +195,6 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         }
     };
     auto lds_ld = [](int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-#if BGX_DBL_BM
     // cnt per-roll jobs (job_of(q), q < cnt <= 15) onto the workgroup's sub-queue
     // when it has room (and every job index is in range), else run here
     auto share = [&](int cnt, auto job_of, bool in_range, const RawJob& cur) {
@@ -221,7 +220,6 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
             }
         }
     };
-#endif
     for (unsigned spin = 0;;) {
         // 1. a queued sub-job first (short; its root's item is done)
         int got = -1;
@@ -281,24 +279,25 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         const int j0 = row * 21;
         if (a.reply_groups && !((a.reply_groups >> grp) & 1)) {
             // tools hook: timing by group
-        } else if (grp > 0 && !BGX_DBL_BM) {
+        } else if (grp > 0 && !DBL) {
             const int j = j0 + dbl_q21(grp);
             if (j < n_jobs) per_roll(j, cur);
-#if BGX_DBL_BM
         } else if (grp > 0) {
-            // the six doubles rolls together (path-mode roots); the rest as per-roll
-            // jobs shared on the sub-queue
-            const JobIn in = decode_job(a, j0, cur);   // the row's root (the dice are not used)
-            uint32_t rest = 0x3Fu;
-            if (in.skip && j0 + 21 <= n_jobs) {
-                for (int d = 1; d <= 6; ++d) begin_emit(a, j0 + dbl_q21(d), 0, fc);
-                rest = 0u;
-            } else if (!in.skip && a.force_tier < 2 && j0 + 21 <= n_jobs) {
-                rest = board_dbl_emit<false>(a, j0, in, M, fc, dcnt[w]);
+            if constexpr (DBL) {
+                // the six doubles rolls together (path-mode roots); the rest as per-roll
+                // jobs shared on the sub-queue
+                const JobIn in = decode_job(a, j0, cur);   // the row's root (the dice are not used)
+                uint32_t rest = 0x3Fu;
+                if (in.skip && j0 + 21 <= n_jobs) {
+                    for (int d = 1; d <= 6; ++d) begin_emit(a, j0 + dbl_q21(d), 0, fc);
+                    rest = 0u;
+                } else if (!in.skip && a.force_tier < 2 && j0 + 21 <= n_jobs) {
+                    rest = board_dbl_emit<false>(a, j0, in, M, fc, dcnt[w]);
+                }
+                if (rest)
+                    share(__popc(rest), [&](int q) { return j0 + dbl_q21(select_bit((uint32_t)rest, q) + 1); },
+                          j0 + 21 <= n_jobs, cur);
             }
-            if (rest) share(__popc(rest), [&](int q) { return j0 + dbl_q21(select_bit((uint32_t)rest, q) + 1); },
-                            j0 + 21 <= n_jobs, cur);
-#endif
         } else {
             const JobIn in = decode_job(a, j0 + 1, cur);   // the row's root (the dice are not used)
             int n = -1, rc = 0;
@@ -582,10 +581,22 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         ev = getenv("BGX_REPLY_BM");
         const bool bm = !ev || atoi(ev) != 0;
         if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT && bm) {
+            // the doubles rolls of a row: one item (board_dbl_emit) when the launch
+            // is large (K = all: the row count is on the device), one item per roll
+            // when it is a short host-counted launch (K = 4: 32,768 rows at 8,192
+            // lanes, where the fewer, longer items balance worse: 0.402 vs 0.365 ms
+            // per launch, against 1.44 vs 1.73 ms for K = all, profiles/round5/).
+            // BGX_REPLY_DBL=0/1 forces it (tests).
+            ev = getenv("BGX_REPLY_DBL");
+            const bool dbl = ev ? atoi(ev) != 0 : a.n_jobs_dev != nullptr;
             int rb = n_cu * per_cup;
-            const int need_r = ((a.n_jobs + 20) / 21 * bgx::REPLY_GROUPS + bgx::PW - 1) / bgx::PW;
+            const int groups = dbl ? bgx::reply_groups<true>() : bgx::reply_groups<false>();
+            const int need_r = ((a.n_jobs + 20) / 21 * groups + bgx::PW - 1) / bgx::PW;
             if (!a.n_jobs_dev && need_r < rb) rb = need_r;
-            hipLaunchKernelGGL(bgx::movegen_reply_kernel, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);
+            if (dbl)
+                hipLaunchKernelGGL(bgx::movegen_reply_kernel<true>, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);
+            else
+                hipLaunchKernelGGL(bgx::movegen_reply_kernel<false>, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);
         } else if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT)
             hipLaunchKernelGGL((bgx::movegen_pool_kernel<bgx::IN_TWOPLY, bgx::OUT_PACKED_FLAT>), dim3(blocks),
                                dim3(64 * bgx::PW), 0, stream, a);

@@ -4,7 +4,7 @@
 // kernel's 16-wave workgroups, its sub-queue and per-roll calls, then the
 // tier-2 block kernel), on candidate rows from a file, with exact-size
 // buffers under AddressSanitizer. Writes every job's record count and rows
-// (in order) to the dump file, so two builds (e.g. BGX_DBL_BM=0 / 1) can be
+// (in order) to the dump file, so two launch forms (BGX_REPLY_DBL=0 / 1) can be
 // compared byte for byte.
 // Usage: reply_emu positions.bin n_roots dump.bin   (positions: 8 packed words + mover, int32)
 #include <cstdio>

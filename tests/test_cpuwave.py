@@ -86,10 +86,10 @@ def _unpack(w):
 
 
 def _reply_vs_oracle(tmp_path, defs, n_cu=2):
-    """The reply launch emulated (default and BGX_DBL_BM=1 builds, extra defs)
-    on self-play and random positions over n_cu emulated CUs: both builds'
-    per-job output byte-identical, and every (board, roll) list the oracle's,
-    order included."""
+    """The reply launch emulated (per-roll doubles items and the board-major
+    doubles kernel, BGX_REPLY_DBL=0 / 1; extra defs) on self-play and random
+    positions over n_cu emulated CUs: both kernels' per-job output
+    byte-identical, and every (board, roll) list the oracle's, order included."""
     orc = pytest.importorskip("oracle")
     from test_gpu_parity import _fuzz_positions, _random_positions
     pos = _fuzz_positions(11, 4) + _random_positions(12, 90)
@@ -100,10 +100,11 @@ def _reply_vs_oracle(tmp_path, defs, n_cu=2):
     rows[:, 8] = opp
     pfile = tmp_path / "pos.bin"
     rows.tofile(pfile)
-    env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0", "EMU_N_CU": str(n_cu)}
     dumps = []
+    exe = _build(tmp_path, "reply_emu.cpp", "reply_emu", list(defs))
     for v in ("0", "1"):
-        exe = _build(tmp_path, "reply_emu.cpp", "reply_emu" + v, ["-DBGX_DBL_BM=" + v, *defs])
+        env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0", "EMU_N_CU": str(n_cu),
+               "BGX_REPLY_DBL": v}
         dump = tmp_path / ("dump" + v + ".bin")
         r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(dump)], capture_output=True, text=True,
                            timeout=900, env=env)
@@ -130,9 +131,10 @@ def test_reply_launch_emulated_equals_oracle(tmp_path):
     """The whole 2-ply reply launch as bgx_reply_moves issues it (reply kernel:
     16-wave workgroups, per-roll calls; then the tier-2 block kernel), emulated
     on the host under AddressSanitizer: every (board, roll) list equals the
-    oracle's movegen (generate_all_moves.py:7-90), order included, for the
-    default build and the board-major doubles build (BGX_DBL_BM=1), whose
-    per-job output is byte-identical to the default's. Built with the
+    oracle's movegen (generate_all_moves.py:7-90), order included, with the
+    per-roll doubles items and with the board-major doubles kernel
+    (BGX_REPLY_DBL=1, the K = all launch's), whose per-job output is
+    byte-identical. Built with the
     workgroup sub-queue off (BGX_REPLY_SUBQ=0: an uncovered root's 15 per-roll
     jobs run on its own wave); the sub-queue is the next test's."""
     _reply_vs_oracle(tmp_path, ["-DBGX_REPLY_SUBQ=0"])
@@ -155,7 +157,7 @@ def test_reply_launch_cross_lane_ops_are_uniform(tmp_path):
     readlane, DPP scans) is reached by all 64 lanes of the wave from the same
     call chain (EMU_SITES build, -O0 -fno-inline): on the GPU one under
     lane-divergent control flow would read inactive lanes. Both builds
-    (default, board-major doubles), with the shipped sub-queue, over 16
+    (per-roll and board-major doubles), with the shipped sub-queue, over 16
     emulated CUs (waves that draw no item sit in the exit test); the emulation
     itself aborts on a kernel that branches around a shuffle (checked with a
     deliberately divergent one). (Round 4's per-lane exit test once left lanes
@@ -188,13 +190,13 @@ def test_reply_launch_cross_lane_ops_are_uniform(tmp_path):
                     "-o", str(exe), "-pthread"], check=True, capture_output=True, text=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "EMU_SITES" in r.stderr
+    exe = tmp_path / "site"
+    subprocess.run(["g++", "-std=c++20", "-O0", "-fno-inline", "-g", "-w", "-DEMU_SITES", *inc, "-x", "c++",
+                    os.path.join(HERE, "cpuwave", "reply_emu.cpp"), "-o", str(exe), "-pthread"], check=True,
+                   capture_output=True, text=True)
     for v in ("0", "1"):
-        exe = tmp_path / ("site" + v)
-        subprocess.run(["g++", "-std=c++20", "-O0", "-fno-inline", "-g", "-w", "-DEMU_SITES", "-DBGX_DBL_BM=" + v,
-                        *inc, "-x", "c++", os.path.join(HERE, "cpuwave", "reply_emu.cpp"), "-o", str(exe),
-                        "-pthread"], check=True, capture_output=True, text=True)
         r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(tmp_path / ("s" + v))], capture_output=True,
-                           text=True, timeout=900, env={**os.environ, "EMU_N_CU": "16"})
+                           text=True, timeout=900, env={**os.environ, "EMU_N_CU": "16", "BGX_REPLY_DBL": v})
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
 
 

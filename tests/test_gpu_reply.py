@@ -35,13 +35,16 @@ def _reply_lists(boards, opp):
     return u8, off.cpu().numpy(), cnt.cpu().numpy()
 
 
-@pytest.mark.parametrize("bm,table", [("1", "0"), ("0", "0"), ("1", "1")])
-def test_reply_moves_vs_oracle(bm, table, monkeypatch):
+@pytest.mark.parametrize("bm,table,dbl", [("1", "0", "0"), ("1", "0", "1"), ("0", "0", "0"), ("1", "1", "0")])
+def test_reply_moves_vs_oracle(bm, table, dbl, monkeypatch):
     """Self-play and random placements (bar 0-2, borne-off checkers, closed
     boards): every (board, roll) list equals the oracle's, order included, in
-    the board-major kernel, the per-roll kernel and (BGX_MG_TEST_TABLE=1:
-    every root through the per-roll hash-table path) the table cross-check."""
+    the board-major kernel with per-roll doubles items (K = 4's) and with the
+    six doubles rolls of a row in one item (BGX_REPLY_DBL=1, K = all's), the
+    per-roll kernel and (BGX_MG_TEST_TABLE=1: every root through the per-roll
+    hash-table path) the table cross-check."""
     monkeypatch.setenv("BGX_REPLY_BM", bm)
+    monkeypatch.setenv("BGX_REPLY_DBL", dbl)
     monkeypatch.setenv("BGX_MG_TEST_TABLE", table)
     monkeypatch.setenv("BGX_MG_FEW", "0")   # the pool / reply kernels (the engine's large launches)
     boards, opp = _positions()
@@ -62,7 +65,8 @@ def test_reply_moves_vs_oracle(bm, table, monkeypatch):
 
 def test_reply_kernels_agree_on_engine_records(weights_seed0, monkeypatch):
     """Engine 2-ply K=4 and K=all: the records of a run do not depend on the
-    reply kernel (board-major vs per-roll)."""
+    reply kernel (board-major -- with per-roll doubles items at K = 4 and the
+    board-major doubles at K = all -- vs per-roll)."""
     from bgx import Engine
     from test_gpu_engine import _by_episode, _collect, _same_runs
 
