@@ -59,6 +59,9 @@ namespace bgx {
 #ifndef BGX_BND
 #define BGX_BND 2          // 1 = the per-roll-round board_nd_records (A/B builds)
 #endif
+#ifndef BGX_REPLY_HEAVY_FIRST
+#define BGX_REPLY_HEAVY_FIRST 0   // 1: reply launch items in doubles-first order (A/B)
+#endif
 #ifndef BGX_POOL_WPE
 #define BGX_POOL_WPE 8
 #endif
@@ -164,7 +167,25 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     M.force_table = a.force_table;
     M.map[l] = 0u;
     const int n_jobs = uniform(job_count(a));
-    const int n_items = (n_jobs + 20) / 21 * REPLY_GROUPS;
+    const int n_rows = (n_jobs + 20) / 21, n_items = n_rows * REPLY_GROUPS;
+    // item -> (row, group). BGX_REPLY_HEAVY_FIRST: the doubles items of every
+    // row first, then the non-doubles items, so a launch ends on the shorter,
+    // more even items; else row-major (each row's groups together)
+    auto item_row = [&](int it, int& grp) -> int {
+        if (BGX_REPLY_HEAVY_FIRST) {
+            const int nd = n_rows * (REPLY_GROUPS - 1);
+            if (it < nd) {
+                const int row = it / (REPLY_GROUPS - 1);
+                grp = 1 + it - (REPLY_GROUPS - 1) * row;
+                return row;
+            }
+            grp = 0;
+            return it - nd;
+        }
+        const int row = it / REPLY_GROUPS;
+        grp = it - REPLY_GROUPS * row;
+        return row;
+    };
     const int G = (int)gridDim.x, b = (int)blockIdx.x;
     const int nk = n_items > b ? (n_items - b + G - 1) / G : 0;
     // the workgroup's sub-queue: the 15 per-roll jobs of a root that
@@ -183,7 +204,10 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     FlatCursor fc;
     int k = w;
     RawJob raw;
-    if (k < nk) raw = fetch_raw(a, (b + k * G) / REPLY_GROUPS * 21);
+    if (k < nk) {
+        int g0;
+        raw = fetch_raw(a, item_row(b + k * G, g0) * 21);
+    }
     // one (row, roll) job as the pool kernel runs it
     auto per_roll = [&](int j, const RawJob& cur) {
         const JobIn in = decode_job(a, j, cur);
@@ -271,9 +295,13 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         if (l == 0) kn = atomicAdd(&next_job, 1);
         kn = uniform(kn);
         const int it = b + k * G;
-        const int row = it / REPLY_GROUPS, grp = it - REPLY_GROUPS * row;
+        int grp;
+        const int row = item_row(it, grp);
         const RawJob cur = raw;
-        if (kn < nk) raw = fetch_raw(a, (b + kn * G) / REPLY_GROUPS * 21);
+        if (kn < nk) {
+            int g0;
+            raw = fetch_raw(a, item_row(b + kn * G, g0) * 21);
+        }
         const int left = (nk - k + PW - 1) / PW;   // items this wave still expects
         fc.left_hint = left;
         const int j0 = row * 21;
