@@ -245,3 +245,51 @@ def test_host_gather_refuses_publish_before_wait():
         assert g.publish(h).wait() == 2
     finally:
         g.close()
+
+
+def test_gather_keeps_a_timed_out_copy(monkeypatch):
+    """A DMA copy that did not finish within its wait (bgx_dma_wait returns
+    BGX_E_STATE and leaves it in flight): the batch is not published, its
+    source arrays stay referenced for the life of the process, and the gather
+    refuses further batches instead of reusing a slot a DMA engine may still
+    write."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    from bgx import _lib, hostgather
+    from bgx.engine import Harvest
+
+    class Fake:
+        def bgx_dma_wait(self, ticket, timeout_ms):
+            return -5
+
+        def bgx_last_error(self):
+            return b"bgx_dma_wait: copy not finished after 1 ms"
+
+    monkeypatch.setattr(_lib, "_lib", Fake())
+    g = hostgather.HostGather(1, 2, hostgather.make_tag(), slot_bytes=4096)
+    try:
+        keep = (torch.ones((1, 16), dtype=torch.int32), torch.ones((2, 12), dtype=torch.int32))
+        p = hostgather.Pending(g, 1, 1, 2, 1, None, dma=(123, 456), keep=keep)
+        with pytest.raises(_lib.BgxError, match="not finished"):
+            p.wait()
+        assert g.broken and p in hostgather.STUCK_COPIES and p.keep is keep
+        assert int(g.ctrl[1][0]) == 0   # never published
+        with pytest.raises(RuntimeError, match="did not finish"):
+            g.publish(Harvest(*keep))
+        hostgather.STUCK_COPIES.remove(p)
+    finally:
+        g.close()
+
+
+def test_device_gather_finds_the_trainer_gpu_by_pci_location():
+    """bgx/devgather.py hands the trainer rank's GPU to its peers as a PCI
+    location, resolved in each peer's own device list: a location
+    no visible device has is an error that names it, not a copy to whatever
+    GPU shares the ordinal."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    from bgx import devgather
+    with pytest.raises(RuntimeError, match="0000:c3:00"):
+        devgather.device_by_pci((0, 0xC3, 0))
