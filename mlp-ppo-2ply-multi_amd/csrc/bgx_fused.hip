@@ -29,6 +29,9 @@
 #include "bgx_mlp.h"
 #include "bgx_movegen.h"
 
+#ifndef BGX_FUSED_NW32
+#define BGX_FUSED_NW32 12   // waves per 32-lane workgroup (12: 3 per SIMD at 168 registers; 8: 2 per SIMD at 256; A/B)
+#endif
 #ifndef BGX_HALF_TICKETS
 #define BGX_HALF_TICKETS 0   // 1: half-lane tickets in a balanced launch's last round (measured slower: DESIGN.md section 9; A/B)
 #endif
@@ -63,7 +66,7 @@ template <int FL> struct FusedTail {
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
 };
 template <int FL> struct FCfg {
-    static constexpr int NW = FL == 32 ? 12 : 8;
+    static constexpr int NW = FL == 32 ? BGX_FUSED_NW32 : 8;
     static constexpr int WPE = NW / 4;                   // waves per SIMD
     // (a 128-slot table with 288-entry frontiers at 12 waves: more tier-2 jobs, not faster)
     static constexpr int P1_S = 256, P1_F = NW > 8 ? 160 : 224, P1_PF = NW > 8 ? 416 : 480;
