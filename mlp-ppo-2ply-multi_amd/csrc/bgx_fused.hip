@@ -32,6 +32,9 @@
 #ifndef BGX_FUSED_NW32
 #define BGX_FUSED_NW32 12   // waves per 32-lane workgroup (12: 3 per SIMD at 168 registers; 8: 2 per SIMD at 256; A/B)
 #endif
+#ifndef BGX_FUSED_NW16
+#define BGX_FUSED_NW16 12   // waves per 16-lane workgroup (fewer lanes than 32 x CUs; 8 measured 6 % slower; A/B)
+#endif
 #ifndef BGX_HALF_TICKETS
 #define BGX_HALF_TICKETS 0   // 1: half-lane tickets in a balanced launch's last round (measured slower: DESIGN.md section 9; A/B)
 #endif
@@ -43,11 +46,12 @@ namespace bgx {
 
 constexpr int PROF_STRIDE = 128;   // u64 words per workgroup slot of the development report (f.prof)
 
-// FL = game lanes per workgroup and NW = waves per workgroup: 16 lanes on 8
-// waves (2 per SIMD, 256 registers) when fewer lanes than 32 x CUs, else 32
-// lanes on 12 waves (3 per SIMD, 168 registers): a step's queue then holds 32
-// jobs, so the long doubles jobs are spread over more short ones, and a third
-// wave per SIMD hides more of each item's latency.
+// FL = game lanes per workgroup and NW = waves per workgroup: 16 lanes when
+// fewer lanes than 32 x CUs, else 32 lanes (a step's queue then holds 32 jobs,
+// so the long doubles jobs are spread over more short ones); both on 12 waves
+// (3 per SIMD, 168 registers): the third wave per SIMD hides more of each
+// item's latency than the spills it costs (32 lanes on 8 waves 270 -> 226 M,
+// 16 lanes on 8 waves at 4,096 lanes 216 -> 203 M).
 // LDS: [scratch | W fragments (resident for the launch) | tail | lane values]
 //  scratch = NW tier-1 slices (the pool kernel's layout, bgx_movegen.hip: a
 //  64-word parent map + a region holding the table-mode or the table-free
@@ -66,7 +70,7 @@ template <int FL> struct FusedTail {
     LaneState st[FL];               // the lanes' state for the whole launch (written back at the end)
 };
 template <int FL> struct FCfg {
-    static constexpr int NW = FL == 32 ? BGX_FUSED_NW32 : 8;
+    static constexpr int NW = FL == 32 ? BGX_FUSED_NW32 : BGX_FUSED_NW16;
     static constexpr int WPE = NW / 4;                   // waves per SIMD
     // (a 128-slot table with 288-entry frontiers at 12 waves: more tier-2 jobs, not faster)
     static constexpr int P1_S = 256, P1_F = NW > 8 ? 160 : 224, P1_PF = NW > 8 ? 416 : 480;
