@@ -1,19 +1,19 @@
 #!/bin/bash
-# The board-major doubles (BGX_DBL_BM=1) after its round-4 fault, guarded:
-# every global write of the movegen kernels and the reply launch's input reads
-# check their index and set an error bit (0x100..0x8000) instead of touching
-# memory out of range (BGX_DBL_GUARD=1; a tripped check comes back from
-# bgx_reply_moves as "overflow flags 0x..."). Built in-tree on the CPU:
+# The board-major doubles reply launch (BGX_REPLY_DBL=1), guarded: every global
+# write of the movegen kernels and the reply launch's input reads check their
+# index and set an error bit (0x100..0x8000) instead of touching memory out of
+# range (BGX_DBL_GUARD=1; a tripped check comes back from bgx_reply_moves as
+# "overflow flags 0x..."). Built in-tree on the CPU:
 #   make -C mlp-ppo-2ply-multi_amd/csrc EXTRA="-DBGX_DBL_GUARD=1" BUILD=build_g OUT=../bgx/libbgx_guard.so
-#   make -C mlp-ppo-2ply-multi_amd/csrc EXTRA="-DBGX_DBL_BM=1 -DBGX_DBL_GUARD=1" BUILD=build_dblg OUT=../bgx/libbgx_dblg.so
-# First the guarded default kernel (the guards themselves must not trip), then
-# ONE reply launch test of the guarded board-major doubles build. Run as the
-# last step of a GPU call: nothing follows it.
+# Runs the reply launch test on the guarded build, per-roll doubles first (the
+# guards themselves must not trip), then board-major. Run as the last step of a
+# GPU call: nothing follows it.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/dblg; mkdir -p $O
 B=$PWD/mlp-ppo-2ply-multi_amd/bgx
-BGX_LIB=$B/libbgx_guard.so timeout -k 10 150 python -u -m pytest "tests/test_gpu_reply.py::test_reply_moves_vs_oracle[1-0]" -x -q --timeout 120 --timeout-method thread > $O/t_guard.log 2>&1 || { tail -30 $O/t_guard.log; exit 1; }
-tail -1 $O/t_guard.log
-BGX_LIB=$B/libbgx_dblg.so timeout -k 10 150 python -u -m pytest "tests/test_gpu_reply.py::test_reply_moves_vs_oracle[1-0]" -x -q --timeout 120 --timeout-method thread > $O/t_dblg.log 2>&1 || { tail -30 $O/t_dblg.log; exit 1; }
-tail -1 $O/t_dblg.log
+T="tests/test_gpu_reply.py::test_reply_moves_vs_oracle[1-0]"
+for dbl in 0 1; do
+  BGX_REPLY_DBL=$dbl BGX_LIB=$B/libbgx_guard.so timeout -k 10 150 python -u -m pytest "$T" -x -q --timeout 120 --timeout-method thread > $O/t_dbl$dbl.log 2>&1 || { tail -30 $O/t_dbl$dbl.log; exit 1; }
+  tail -1 $O/t_dbl$dbl.log
+done

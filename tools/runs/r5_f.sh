@@ -1,7 +1,9 @@
 #!/bin/bash
 # round 5: the board-major doubles build (BGX_DBL_BM=1, unguarded) after its
 # guarded build passed the reply test: the reply and 2-ply engine tests on it,
-# then the 2-ply legs A/B against the in-tree (per-roll doubles) build
+# then the 2-ply legs A/B against the in-tree (per-roll doubles) build.
+# Record of a run: the build flag has since become the runtime switch
+# BGX_REPLY_DBL, so this script no longer builds.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r5f; mkdir -p $O
