@@ -382,15 +382,17 @@ def roofline_for(d, tm, leg):
     el = d["elapsed_s"]
     mg_ms, mlp_ms = tm["movegen_ms"], tm["mlp_ms"]
     out = {}
-    # boards movegen wrote = value rows minus the lanes' own rows (one per lane step)
-    mg_rows = d["value_rows"] - d["env_steps"]
+    # boards movegen wrote = value rows minus the lanes' own rows (one per lane
+    # step) and the reply launch's unwritten gap rows
+    rec_rows = d["value_rows"] - d.get("gap_rows", 0)
+    mg_rows = rec_rows - d["env_steps"]
     mg_bytes = MOVEGEN_BYTES_PER_JOB * d["movegen_jobs"] + MOVEGEN_BYTES_PER_ROW * mg_rows
     mg_launch = mg_ms / max(1, tm["movegen_launches"])
     out["movegen"] = {"bound": "hbm", "achieved": mg_bytes / max(1, tm["movegen_launches"]) / (mg_launch * 1e-3) / 1e9,
                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "avg_launch_ms": mg_launch,
                       "launches": tm["movegen_launches"], "share_of_wall": mg_ms * 1e-3 / el}
     mlp_launch = mlp_ms / max(1, tm["mlp_launches"])
-    mlp_flop = MLP_FLOP_PER_ROW * d["value_rows"] / max(1, tm["mlp_launches"])
+    mlp_flop = MLP_FLOP_PER_ROW * rec_rows / max(1, tm["mlp_launches"])   # gap rows: executed, not counted
     out["mlp"] = {"bound": "mfma", "achieved": mlp_flop / (mlp_launch * 1e-3) / 1e12, "peak": FP16_DENSE_PEAK_TFS,
                   "unit": "TFLOP/s", "avg_launch_ms": mlp_launch, "launches": tm["mlp_launches"],
                   "share_of_wall": mlp_ms * 1e-3 / el}
@@ -505,6 +507,9 @@ def main():
                 "value_rows_per_s": sum_over_ranks(d_["value_rows"], world) / el_,
                 "movegen_jobs_per_s": sum_over_ranks(d_["movegen_jobs"], world) / el_,
                 "fallback_jobs": int(sum_over_ranks(d_["fallback_jobs"], world)),
+                # 2-ply: reply rows the movegen reserved but left unwritten (the MLP
+                # evaluates them; the algorithmic figures below leave them out)
+                "gap_rows_frac": sum_over_ranks(d_["gap_rows"], world) / max(1, sum_over_ranks(d_["value_rows"], world)),
                 "roofline": roof_, "kernels": kern_, "desync_steps": desync,
                 "seed": args.seed if seed is None else seed}
         if world > 1:
@@ -558,7 +563,7 @@ def main():
                                      leg(2, 0, args.lanes, args.kall_steps, 5,
                                          min(args.kall_steps, args.timing_steps, 10), "2ply_kall"))
         extra["two_ply_kall"]["reply_boards_per_decision"] = \
-            (d3["value_rows"] - 2 * d3["env_steps"]) / max(1, d3["decisions"])
+            (d3["value_rows"] - d3["gap_rows"] - 2 * d3["env_steps"]) / max(1, d3["decisions"])
     if args.ply == 1 and world == 1 and args.config1_steps > 0 and args.lanes != 4096:
         c1, _ = (protocol(1, 4, 4096, 100, min(args.config1_steps, args.timing_steps), "1ply", 600) if proto else
                  leg(1, 4, 4096, args.config1_steps, 100, min(args.config1_steps, args.timing_steps), "1ply"))
@@ -590,6 +595,7 @@ def main():
             "world_size": world, "env_steps_per_rank": head["env_steps_per_rank"],
             "decisions_per_s": head["decisions_per_s"], "episodes_per_s": head["episodes_per_s"],
             "value_rows_per_s": head["value_rows_per_s"], "fallback_jobs": head["fallback_jobs"],
+            "gap_rows_frac": head["gap_rows_frac"],
             "roofline": head["roofline"], "kernels": head["kernels"], "cpu_baseline": cpu,
             "seed": head["seed"], "protocol": head.get("protocol"),
             "episodes_per_s_note": "device-side: episodes finished and harvested on the GPU per second"

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 8
+#define BGX_ABI_VERSION 9
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -245,6 +245,8 @@ typedef struct bgx_stats {
     uint64_t value_rows;    /* boards evaluated by the value MLP */
     uint64_t movegen_jobs;  /* (board, dice) move generations */
     uint64_t fallback_jobs; /* doubles jobs re-run on the global-memory path */
+    uint64_t gap_rows;      /* of value_rows: 2-ply reply rows reserved in per-wave chunks but left
+                               unwritten (the reply MLP evaluates them; no record reads them) */
 } bgx_stats;
 int bgx_get_stats(bgx_engine* e, bgx_stats* out);  /* synchronizes */
 

@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("BGX_LIB", os.path.join(_HERE, "libbgx.so"))
 c_int, c_float, c_double, c_u64, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                              ctypes.c_uint64, ctypes.c_void_p)
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class BgxError(RuntimeError):
@@ -45,7 +45,7 @@ class HarvestInfo(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("env_steps", c_u64), ("decisions", c_u64), ("episodes", c_u64),
-                ("value_rows", c_u64), ("movegen_jobs", c_u64), ("fallback_jobs", c_u64)]
+                ("value_rows", c_u64), ("movegen_jobs", c_u64), ("fallback_jobs", c_u64), ("gap_rows", c_u64)]
 
 
 # every entry point declared in include/bgx.h: name -> (restype, argtypes)

@@ -162,6 +162,9 @@ struct bgx_engine {
 
 namespace {
 constexpr int C_EP = 3, C_ERR = 4, C_FLAT = 8, C_REPLY = 9, C_OVF = 10, C_OVF2 = 11;
+// stats words: [0..7] counters (bgx_get_stats), then the top-5 launch's per-wave
+// reply-record counts
+constexpr int kStatWords = 8 + bgx::T5_WAVES;
 constexpr int C_BUDGET = 12;   // [12..15]: the balanced fused launch's lane-step and finished-workgroup counters (u64)
 }
 
@@ -921,7 +924,7 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
             m.feat_scale = net->feat_scale;
             if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
         }
-        if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, sample_k, seed, nullptr, s) != hipSuccess)
+        if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, sample_k, seed, nullptr, nullptr, s) != hipSuccess)
             rc = BGX_E_HIP;
         if (!rc && bgx_launch_two_ply_reduce(jv, n, d_out, s) != hipSuccess) rc = BGX_E_HIP;
         unsigned flags = 0;
@@ -1142,7 +1145,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
         ALLOC(e->cand_off, L);
         ALLOC(e->cand_cnt, L);
         ALLOC(e->ctr, 16);
-        ALLOC(e->stats, 8);
+        ALLOC(e->stats, kStatWords);
         ALLOC(d.player, L);
         ALLOC(d.dice, 2 * L);
         ALLOC(d.step, L);
@@ -1206,7 +1209,7 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             bgx_engine_destroy(e);
             return rc;
         }
-        if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, 64) != hipSuccess ||
+        if (hipMemset(e->ctr, 0, 64) != hipSuccess || hipMemset(e->stats, 0, kStatWords * sizeof(unsigned long long)) != hipSuccess ||
             (e->fh_ctr && hipMemset(e->fh_ctr, 0, (3 * bgx_engine::NHB + 1) * sizeof(unsigned long long)) != hipSuccess)) {
             bgx_engine_destroy(e);
             return fail(BGX_E_HIP, "hipMemset failed");
@@ -1417,10 +1420,10 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             const uint64_t skey = e->cfg.seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(e->cfg.lane_base + 1));
             if (e->cfg.k_top == 4) {
                 HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, L * 4 * 21, nullptr, 0, L * 4 * 21,
-                                        e->job_val, e->cfg.reply_sample, skey, e->stats, s));
+                                        e->job_val, e->cfg.reply_sample, skey, e->stats, e->stats + 8, s));
             } else {
                 HIP_TRY(bgx_launch_top5(e->reply_V, e->job_off, e->job_cnt, 0, e->ctr + C_FLAT, 21, e->jobs_cap,
-                                        e->job_val, e->cfg.reply_sample, skey, e->stats, s));
+                                        e->job_val, e->cfg.reply_sample, skey, e->stats, e->stats + 8, s));
             }
         }
         HIP_TRY(bgx_launch_select(&e->d, s));   // select + env step (one launch)
@@ -1634,8 +1637,9 @@ int bgx_get_stats(bgx_engine* e, bgx_stats* out) {
         if (!e || !out) return fail(BGX_E_ARG, "bgx_get_stats: null pointer");
         HIP_TRY(hipSetDevice(e->device));
         if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
-        unsigned long long st[8];
-        HIP_TRY(hipMemcpy(st, e->stats, sizeof(st), hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> st(kStatWords);
+        HIP_TRY(hipMemcpy(st.data(), e->stats, kStatWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (int i = 8; i < kStatWords; ++i) st[7] += st[i];   // the top-5 launch's per-wave record counts
         // decisions = records written, episodes = games finished: the lanes' own counters
         const int L = e->cfg.lanes;
         std::vector<uint32_t> rec(L), epi(L);
@@ -1652,6 +1656,7 @@ int bgx_get_stats(bgx_engine* e, bgx_stats* out) {
         out->value_rows = st[3];
         out->movegen_jobs = st[4];
         out->fallback_jobs = st[5];
+        out->gap_rows = st[6] - st[7];   // 2-ply reply rows reserved minus the records written into them
         return BGX_OK;
     });
 }

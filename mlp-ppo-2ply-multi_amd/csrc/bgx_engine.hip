@@ -60,6 +60,7 @@ __global__ __launch_bounds__(256) void select_step_kernel(EngineDev e) {
         unsigned long long rows = (unsigned long long)e.L + fc, jobs = (unsigned long long)e.L;
         if (e.ply == 2) {
             rows += *e.reply_count;
+            atomicAdd(e.stats + 6, (unsigned long long)*e.reply_count);   // reply rows (gaps included)
             jobs += e.k_top == 0 ? 21ull * fc : (unsigned long long)e.n_jobs2;
         }
         atomicAdd(e.stats + 0, (unsigned long long)e.L);
@@ -224,7 +225,8 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    const unsigned* __restrict__ n_units_dev,
                                                    int jobs_per_unit, int max_jobs, float* __restrict__ out,
                                                    int sample_k, uint64_t skey,
-                                                   const unsigned long long* __restrict__ salt_dev) {
+                                                   const unsigned long long* __restrict__ salt_dev,
+                                                   unsigned long long* __restrict__ rec_acc) {
     constexpr int JW = 64 / T5_GL;   // jobs per wave iteration
     int nj = n_jobs;
     if (n_units_dev) nj += (int)(*n_units_dev) * jobs_per_unit;
@@ -239,6 +241,7 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
     auto job_of = [&](int it) { return (JW * (it / 21) + q) * 21 + it % 21; };
     int itr = wave;
     int cn = 0, on = 0;
+    unsigned long long recs = 0;   // the jobs' records (rec_acc: the engine's reply-record count)
     if (itr < n_it) {
         const int j0 = job_of(itr);
         if (j0 < nj) {
@@ -258,6 +261,7 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                 on = job_off[jn];
             }
         }
+        recs += (unsigned long long)c;
         const bool samp = sample_k > 0 && c > sample_k && c <= 1024 && small_double(j);
         u32x4 pk = {0u, 0u, 0u, 0u};
         if (samp) pk = philox(skey, 0x2B1A000000000000ull ^ salt, (uint64_t)j);
@@ -298,6 +302,15 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
             if (who == gl) { t[0] = t[1]; t[1] = t[2]; t[2] = t[3]; t[3] = t[4]; t[4] = -INFINITY; }
         }
         if (live && gl == 0) out[j] = m ? s / (float)m : 0.0f;
+    }
+    if (rec_acc && wave < T5_WAVES) {
+        // every lane of a 4-lane group counted its job's c: lanes gl == 0 only.
+        // One slot per wave, a plain add (the grid is the same every launch of an
+        // engine; a same-address atomic per wave cost ~75 us per launch)
+        unsigned long long r = gl == 0 ? recs : 0ull;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) r += __shfl_xor(r, off, 64);
+        if (lane_id() == 0 && r) rec_acc[wave] += r;
     }
 }
 
@@ -462,12 +475,13 @@ extern "C" hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t strea
 extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt,
                                       int n_jobs, const unsigned* n_units_dev, int jobs_per_unit,
                                       int max_jobs, float* out, int sample_k, uint64_t skey,
-                                      const unsigned long long* salt_dev, hipStream_t stream) {
+                                      const unsigned long long* salt_dev, unsigned long long* rec_acc,
+                                      hipStream_t stream) {
     if (max_jobs <= 0) return hipSuccess;
     int blocks = (max_jobs + 4 * 16 - 1) / (4 * 16);   // 16 jobs per wave, 4 waves per block
-    if (blocks > 2048) blocks = 2048;                   // 8 waves per SIMD on 256 CUs, then loop
+    if (blocks > bgx::T5_WAVES / 4) blocks = bgx::T5_WAVES / 4;   // 8 waves per SIMD on 256 CUs, then loop
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
-                       n_units_dev, jobs_per_unit, max_jobs, out, sample_k, skey, salt_dev);
+                       n_units_dev, jobs_per_unit, max_jobs, out, sample_k, skey, salt_dev, rec_acc);
     return hipGetLastError();
 }
 extern "C" hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out,

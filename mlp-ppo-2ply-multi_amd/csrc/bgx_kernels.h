@@ -58,6 +58,8 @@ struct MovegenArgs {
                                  //   reply items of these groups (bit 0: non-doubles, bit d: (d, d)); 0 = all;
                                  //   0x80: leave roots board_nd_records does not cover out; 0x100: treat
                                  //   every root as not covered
+    int dbl_tail64;              // set by the launcher (board-major doubles reply launch): the last
+                                 //   dbl_tail64 / 64 of the rows run one item per doubles roll
     unsigned* err_flags;
 };
 
@@ -214,6 +216,10 @@ struct TrainArgs {
     double* metrics;             // [5] += loss, post-clip grad norm, |td| mean, V mean, reward sum (per episode)
 };
 
+// the 2-ply top-5 launch: at most this many waves (2,048 blocks of 4), each
+// with its own record-count slot (bgx_launch_top5's rec_acc)
+constexpr int T5_WAVES = 2048 * 4;
+
 }  // namespace bgx
 
 extern "C" {
@@ -236,7 +242,9 @@ hipError_t bgx_launch_topk(const bgx::EngineDev* e, hipStream_t stream);
 hipError_t bgx_launch_select(const bgx::EngineDev* e, hipStream_t stream);   // select + env step
 hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, const int32_t* job_cnt, int n_jobs,
                            const unsigned* n_units_dev, int jobs_per_unit, int max_jobs, float* out,
-                           int sample_k, uint64_t skey, const unsigned long long* salt_dev, hipStream_t stream);
+                           int sample_k, uint64_t skey, const unsigned long long* salt_dev,
+                           unsigned long long* rec_acc, hipStream_t stream);   // rec_acc[wave] += its jobs' records
+                                                                     // (bgx::T5_WAVES slots, or null)
 hipError_t bgx_launch_two_ply_reduce(const float* job_val, int n, double* out, hipStream_t stream);
 hipError_t bgx_launch_td0(const bgx::TrainArgs* args, hipStream_t stream);
 // harvest: episode offsets / totals (info[4] on the device, hinfo[4] host-mapped

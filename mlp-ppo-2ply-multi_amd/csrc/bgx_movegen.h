@@ -481,7 +481,21 @@ BGX_DEV void emit_one(const MovegenArgs& a, int j, const Root& R, const Node& n,
 // (base2, left2): the larger remainder of an earlier chunk, kept when a request
 // did not fit it (a 2-ply row block of ~200 rows would otherwise leave up to a
 // block's worth of gap rows per chunk, which the reply MLP evaluates)
-struct FlatCursor { int base = 0, left = 0, left_hint = -1, base2 = 0, left2 = 0; };
+// wg (the reply launch): requests that neither remainder holds are served from
+// a workgroup-level chunk in LDS (WgRows) instead of a global atomic per wave
+// chunk; a wave's unused chunk tail at the end of the launch was a gap row
+// block of up to flat_chunk rows per wave (14 % of a K = 4 launch's rows, 7 %
+// at K = all), while the workgroup sizes its chunks by its remaining items and
+// leaves one small tail per workgroup.
+struct WgRows {
+    unsigned long long span;   // current chunk: next free row (low 32 bits), end (high 32)
+    unsigned used;             // rows handed to requests so far
+    int next, done, items;     // the workgroup's items: claimed (its LDS item counter), finished, all
+};
+struct FlatCursor {
+    int base = 0, left = 0, left_hint = -1, base2 = 0, left2 = 0;
+    WgRows* wg = nullptr;   // LDS, or null: per-wave chunks from the global counter
+};
 
 // n rows from the cursor's current or kept remainder; false: neither holds them
 BGX_DEV bool cursor_take(FlatCursor& fc, int n, int& base) {
@@ -509,11 +523,108 @@ BGX_DEV void cursor_new_chunk(FlatCursor& fc, int base, int n, int grab) {
     fc.left = grab - n;
 }
 
+// n rows from the workgroup's chunk (lane 0 decides, the result is broadcast);
+// -1: the flat buffer is full (flagged). A request the chunk cannot hold
+// locks the span (bit 31 of its end), refills it with a global reservation
+// sized by the workgroup's progress -- rows per item so far x (items not yet
+// claimed + half the items in flight), between max(n, 64) and 8 x flat_chunk,
+// so the chunks shrink as the workgroup's items run out -- and unlocks it;
+// requests that meet the lock wait for the new chunk (one refill at a time:
+// concurrent refills each kept a chunk, 16 per workgroup at a launch's start).
+// The replaced chunk's tail becomes the refilling wave's own remainder.
+constexpr unsigned WG_LOCK = 0x80000000u;
+BGX_DEV int wg_take(const MovegenArgs& a, int n, FlatCursor& fc) {
+    int b = 0, rb = 0, rl = 0;
+    if (lane_id() == 0) {
+        WgRows* g = fc.wg;
+        unsigned long long s = __hip_atomic_load(&g->span, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (unsigned spin = 0;;) {
+            const unsigned nx = (unsigned)s, en = (unsigned)(s >> 32);
+            if (en & WG_LOCK) {   // another wave is refilling
+                if (++spin >= (1u << 24)) {   // bounded
+                    atomicOr(a.err_flags, BGX_ERRF_WAIT_BOUND);
+                    b = -1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                s = __hip_atomic_load(&g->span, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                continue;
+            }
+            if (nx + (unsigned)n <= en) {
+                const unsigned long long prev = atomicCAS(&g->span, s, ((unsigned long long)en << 32) | (nx + n));
+                if (prev == s) {
+                    b = (int)nx;
+                    break;
+                }
+                s = prev;
+                continue;
+            }
+            const unsigned long long lk = ((unsigned long long)(en | WG_LOCK) << 32) | nx;
+            const unsigned long long prev = atomicCAS(&g->span, s, lk);
+            if (prev != s) {
+                s = prev;
+                continue;
+            }
+            const int items = g->items;
+            int claimed = __hip_atomic_load(&g->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (claimed > items) claimed = items;
+            const int done = __hip_atomic_load(&g->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int flight = claimed > done ? claimed - done : 0;
+            const unsigned used = __hip_atomic_load(&g->used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // prior: ~107 records per item at K = 4 (8,192 lanes, 12/64 per-roll tail)
+            const float per_item = used ? (float)used / (float)(2 * done + flight + 1) * 2.0f : 128.0f;
+            const int cap = 8 * a.flat_chunk;
+            const float want_f = per_item * (float)(2 * (items - claimed) + flight + 1) * 0.5f;
+            int want = want_f > (float)cap ? cap : (int)want_f;
+            if (want < 64) want = 64;
+            const int grab = n > want ? n : want;
+            const int gb = (int)atomicAdd(a.flat_count, (unsigned)grab);
+            if (gb + grab > a.flat_cap) {
+                atomicOr(a.err_flags, BGX_ERRF_FLAT_OVERFLOW);
+                __hip_atomic_store(&g->span, ((unsigned long long)en << 32) | en, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                b = -1;
+                break;
+            }
+            __hip_atomic_store(&g->span, ((unsigned long long)(unsigned)(gb + grab) << 32) | (unsigned)(gb + n),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            b = gb;
+            rb = (int)nx;   // the replaced chunk's tail: this wave's now
+            rl = (int)(en - nx);
+            break;
+        }
+        if (b >= 0) atomicAdd(&g->used, (unsigned)n);
+    }
+    b = uniform(b);
+    rb = uniform(rb);
+    rl = uniform(rl);
+    if (b < 0) {
+        fc.left = fc.left2 = 0;
+        return -1;
+    }
+    // keep the larger two of (current, kept, new) remainders
+    if (rl > fc.left) {
+        if (fc.left > fc.left2) {
+            fc.base2 = fc.base;
+            fc.left2 = fc.left;
+        }
+        fc.base = rb;
+        fc.left = rl;
+    } else if (rl > fc.left2) {
+        fc.base2 = rb;
+        fc.left2 = rl;
+    }
+    return b;
+}
+
 // reserve output space once the job's record count is known; returns base (-1: overflow)
 BGX_DEV int begin_emit(const MovegenArgs& a, int j, int n, FlatCursor& fc) {
     int base = 0;
     if (a.out_mode == OUT_PACKED_FLAT) {
-        if (!cursor_take(fc, n, base)) {
+        if (cursor_take(fc, n, base)) {
+        } else if (fc.wg) {
+            base = wg_take(a, n, fc);
+        } else {
             // chunk = min(flat_chunk, 32 rows per job this wave still has), at least n
             const int left_jobs =
                 fc.left_hint >= 0 ? fc.left_hint : (job_count(a) - j + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -1617,6 +1728,7 @@ BGX_DEV int board_nd_records2(const Root& R, uint32_t* map, uint32_t* list, uint
 BGX_DEV int reserve_flat(const MovegenArgs& a, int n, FlatCursor& fc, int want) {
     int base = 0;
     if (cursor_take(fc, n, base)) return base;
+    if (fc.wg) return wg_take(a, n, fc);
     if (want > a.flat_chunk) want = a.flat_chunk;
     const int grab = n > want ? n : want;
     if (lane_id() == 0) base = (int)atomicAdd(a.flat_count, (unsigned)grab);

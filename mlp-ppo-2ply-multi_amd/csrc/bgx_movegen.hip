@@ -59,8 +59,11 @@ namespace bgx {
 #ifndef BGX_BND
 #define BGX_BND 2          // 1 = the per-roll-round board_nd_records (A/B builds)
 #endif
-#ifndef BGX_REPLY_HEAVY_FIRST
-#define BGX_REPLY_HEAVY_FIRST 0   // 1: reply launch items in doubles-first order (A/B)
+#ifndef BGX_REPLY_DBL_TAIL
+#define BGX_REPLY_DBL_TAIL 12   // board-major doubles launch: 64ths of the rows left in per-roll items
+#endif
+#ifndef BGX_REPLY_WG
+#define BGX_REPLY_WG 1   // A/B builds: 0 = the reply launch's waves reserve rows in per-wave chunks
 #endif
 #ifndef BGX_POOL_WPE
 #define BGX_POOL_WPE 8
@@ -139,19 +142,21 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
 // (job order within a row's block is the DICE_ROLLS order); overflowing
 // per-roll jobs go to tier 2 as before.
 // DBL (the launch picks it, bgx_launch_movegen): a row's six doubles rolls in
-// one item (board_dbl_emit), groups 0..1; otherwise one item per doubles roll,
-// groups 0..6.
-template <bool DBL> constexpr int reply_groups() { return DBL ? 2 : 7; }
+// one item (board_dbl_emit), groups 0..1, except for the last a.dbl_tail64 / 64
+// of the rows, which keep one item per doubles roll (groups 0..6): a
+// workgroup's items end on the short per-roll ones, so its waves finish
+// together. Not DBL: every row in per-roll items.
 constexpr int REPLY_SUBQ = 1024;   // sub-queue entries per workgroup (4 KB of LDS: 2 x 68 KB per CU)
 template <bool DBL>
 __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POOL_WPE))) void movegen_reply_kernel(
     MovegenArgs a0) {
-    constexpr int REPLY_GROUPS = reply_groups<DBL>();
     MovegenArgs a = a0;
     a.in_mode = IN_TWOPLY;
     a.out_mode = OUT_PACKED_FLAT;
     __shared__ __attribute__((aligned(16))) unsigned long long smem[PW * PSL / 8];
-    __shared__ int next_job;
+    __shared__ WgRows wgr;   // the workgroup's item counters and output rows (FlatCursor::wg)
+    int& next_job = wgr.next;
+    int& items_done = wgr.done;
     const int w = (int)threadIdx.x >> 6, l = lane_id();
     uint32_t* sl = (uint32_t*)(smem + (size_t)w * (PSL / 8));
     Mem M;
@@ -167,24 +172,27 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     M.force_table = a.force_table;
     M.map[l] = 0u;
     const int n_jobs = uniform(job_count(a));
-    const int n_rows = (n_jobs + 20) / 21, n_items = n_rows * REPLY_GROUPS;
-    // item -> (row, group). BGX_REPLY_HEAVY_FIRST: the doubles items of every
-    // row first, then the non-doubles items, so a launch ends on the shorter,
-    // more even items; else row-major (each row's groups together)
-    auto item_row = [&](int it, int& grp) -> int {
-        if (BGX_REPLY_HEAVY_FIRST) {
-            const int nd = n_rows * (REPLY_GROUPS - 1);
-            if (it < nd) {
-                const int row = it / (REPLY_GROUPS - 1);
-                grp = 1 + it - (REPLY_GROUPS - 1) * row;
-                return row;
-            }
-            grp = 0;
-            return it - nd;
+    const int n_rows = (n_jobs + 20) / 21;
+    // rows [0, head): items (row, 0) and (row, all doubles); rows [head, n_rows):
+    // items (row, 0..6). Row-major, so a row's items run close together.
+    int tail = n_rows;
+    if constexpr (DBL) {
+        const int t64 = a.dbl_tail64 < 0 ? 0 : a.dbl_tail64 > 64 ? 64 : a.dbl_tail64;
+        tail = (int)(((long long)n_rows * t64 + 63) >> 6);
+    }
+    const int head = n_rows - tail, n_items = 2 * head + 7 * tail;
+    // item -> (row, group); grp 1..6 with whole = the six doubles rolls at once
+    auto item_row = [&](int it, int& grp, bool& whole) -> int {
+        if (it < 2 * head) {
+            grp = it & 1;
+            whole = grp != 0;
+            return it >> 1;
         }
-        const int row = it / REPLY_GROUPS;
-        grp = it - REPLY_GROUPS * row;
-        return row;
+        it -= 2 * head;
+        const int q = it / 7;
+        grp = it - 7 * q;
+        whole = false;
+        return head + q;
     };
     const int G = (int)gridDim.x, b = (int)blockIdx.x;
     const int nk = n_items > b ? (n_items - b + G - 1) / G : 0;
@@ -193,20 +201,25 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
     // 0 until the pushing wave has written it) instead of running in a row on
     // one wave (at ~13 us per job that wave ends ~190 us after the others)
     __shared__ int subq[REPLY_SUBQ];
-    __shared__ int sub_res, sub_head, items_done;
+    __shared__ int sub_res, sub_head;
     __shared__ uint32_t dcnt[DBL ? PW : 1][8];   // board_dbl_emit's per-die child counts, per wave
     for (int i = (int)threadIdx.x; i < REPLY_SUBQ; i += 64 * PW) subq[i] = 0;
     if (threadIdx.x == 0) {
         next_job = PW;
         sub_res = sub_head = items_done = 0;
+        wgr.span = 0ull;
+        wgr.used = 0u;
+        wgr.items = nk;
     }
     __syncthreads();
     FlatCursor fc;
+    if (BGX_REPLY_WG) fc.wg = &wgr;
     int k = w;
     RawJob raw;
     if (k < nk) {
         int g0;
-        raw = fetch_raw(a, item_row(b + k * G, g0) * 21);
+        bool w0;
+        raw = fetch_raw(a, item_row(b + k * G, g0, w0) * 21);
     }
     // one (row, roll) job as the pool kernel runs it
     auto per_roll = [&](int j, const RawJob& cur) {
@@ -296,18 +309,20 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
         kn = uniform(kn);
         const int it = b + k * G;
         int grp;
-        const int row = item_row(it, grp);
+        bool whole;
+        const int row = item_row(it, grp, whole);
         const RawJob cur = raw;
         if (kn < nk) {
             int g0;
-            raw = fetch_raw(a, item_row(b + kn * G, g0) * 21);
+            bool w0;
+            raw = fetch_raw(a, item_row(b + kn * G, g0, w0) * 21);
         }
         const int left = (nk - k + PW - 1) / PW;   // items this wave still expects
         fc.left_hint = left;
         const int j0 = row * 21;
         if (a.reply_groups && !((a.reply_groups >> grp) & 1)) {
             // tools hook: timing by group
-        } else if (grp > 0 && !DBL) {
+        } else if (grp > 0 && !whole) {
             const int j = j0 + dbl_q21(grp);
             if (j < n_jobs) per_roll(j, cur);
         } else if (grp > 0) {
@@ -609,17 +624,19 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
         ev = getenv("BGX_REPLY_BM");
         const bool bm = !ev || atoi(ev) != 0;
         if (a.in_mode == bgx::IN_TWOPLY && a.out_mode == bgx::OUT_PACKED_FLAT && bm) {
-            // the doubles rolls of a row: one item (board_dbl_emit) when the launch
-            // is large (K = all: the row count is on the device), one item per roll
-            // when it is a short host-counted launch (K = 4: 32,768 rows at 8,192
-            // lanes, where the fewer, longer items balance worse: 0.402 vs 0.365 ms
-            // per launch, against 1.44 vs 1.73 ms for K = all, profiles/round5/).
-            // BGX_REPLY_DBL=0/1 forces it (tests).
+            // the doubles rolls of a row: one item (board_dbl_emit), except for the
+            // last BGX_REPLY_DBL_TAIL / 64 of the rows, whose six rolls are six
+            // items, so a workgroup ends on short items. K = 4 at 8,192 lanes (32,768
+            // rows over 512 workgroups): 1.590 ms per step with per-roll items only,
+            // 1.667 with none of them, 1.532-1.536 with 10-24 / 64; K = all: within
+            // noise (7.95-7.99 ms; tools/runs/r5_l.sh, r5_m.sh). BGX_REPLY_DBL=0:
+            // per-roll doubles items only (tests, A/B).
             ev = getenv("BGX_REPLY_DBL");
-            const bool dbl = ev ? atoi(ev) != 0 : a.n_jobs_dev != nullptr;
+            const bool dbl = !ev || atoi(ev) != 0;
+            ev = getenv("BGX_REPLY_DBL_TAIL");
+            a.dbl_tail64 = ev ? atoi(ev) : BGX_REPLY_DBL_TAIL;
             int rb = n_cu * per_cup;
-            const int groups = dbl ? bgx::reply_groups<true>() : bgx::reply_groups<false>();
-            const int need_r = ((a.n_jobs + 20) / 21 * groups + bgx::PW - 1) / bgx::PW;
+            const int need_r = ((a.n_jobs + 20) / 21 * 7 + bgx::PW - 1) / bgx::PW;   // at most 7 items per row
             if (!a.n_jobs_dev && need_r < rb) rb = need_r;
             if (dbl)
                 hipLaunchKernelGGL(bgx::movegen_reply_kernel<true>, dim3(rb), dim3(64 * bgx::PW), 0, stream, a);

@@ -87,7 +87,8 @@ def _unpack(w):
 
 def _reply_vs_oracle(tmp_path, defs, n_cu=2):
     """The reply launch emulated (per-roll doubles items and the board-major
-    doubles kernel, BGX_REPLY_DBL=0 / 1; extra defs) on self-play and random
+    doubles kernel, BGX_REPLY_DBL=0 / 1, the latter with half its rows in
+    per-roll items, BGX_REPLY_DBL_TAIL=32; extra defs) on self-play and random
     positions over n_cu emulated CUs: both kernels' per-job output
     byte-identical, and every (board, roll) list the oracle's, order included."""
     orc = pytest.importorskip("oracle")
@@ -104,7 +105,7 @@ def _reply_vs_oracle(tmp_path, defs, n_cu=2):
     exe = _build(tmp_path, "reply_emu.cpp", "reply_emu", list(defs))
     for v in ("0", "1"):
         env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0", "EMU_N_CU": str(n_cu),
-               "BGX_REPLY_DBL": v}
+               "BGX_REPLY_DBL": v, "BGX_REPLY_DBL_TAIL": "32"}
         dump = tmp_path / ("dump" + v + ".bin")
         r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(dump)], capture_output=True, text=True,
                            timeout=900, env=env)
@@ -157,7 +158,8 @@ def test_reply_launch_cross_lane_ops_are_uniform(tmp_path):
     readlane, DPP scans) is reached by all 64 lanes of the wave from the same
     call chain (EMU_SITES build, -O0 -fno-inline): on the GPU one under
     lane-divergent control flow would read inactive lanes. Both builds
-    (per-roll and board-major doubles), with the shipped sub-queue, over 16
+    (per-roll and board-major doubles, half its rows per roll), with the
+    shipped sub-queue, over 16
     emulated CUs (waves that draw no item sit in the exit test); the emulation
     itself aborts on a kernel that branches around a shuffle (checked with a
     deliberately divergent one). (Round 4's per-lane exit test once left lanes
@@ -196,7 +198,8 @@ def test_reply_launch_cross_lane_ops_are_uniform(tmp_path):
                    capture_output=True, text=True)
     for v in ("0", "1"):
         r = subprocess.run([str(exe), str(pfile), str(len(pos)), str(tmp_path / ("s" + v))], capture_output=True,
-                           text=True, timeout=900, env={**os.environ, "EMU_N_CU": "16", "BGX_REPLY_DBL": v})
+                           text=True, timeout=900, env={**os.environ, "EMU_N_CU": "16", "BGX_REPLY_DBL": v,
+                                                        "BGX_REPLY_DBL_TAIL": "32"})
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
 
 

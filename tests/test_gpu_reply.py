@@ -35,16 +35,19 @@ def _reply_lists(boards, opp):
     return u8, off.cpu().numpy(), cnt.cpu().numpy()
 
 
-@pytest.mark.parametrize("bm,table,dbl", [("1", "0", "0"), ("1", "0", "1"), ("0", "0", "0"), ("1", "1", "0")])
-def test_reply_moves_vs_oracle(bm, table, dbl, monkeypatch):
+@pytest.mark.parametrize("bm,table,dbl,tail", [("1", "0", "1", "12"), ("1", "0", "1", "0"), ("1", "0", "0", "12"),
+                                               ("0", "0", "0", "12"), ("1", "1", "0", "12")])
+def test_reply_moves_vs_oracle(bm, table, dbl, tail, monkeypatch):
     """Self-play and random placements (bar 0-2, borne-off checkers, closed
     boards): every (board, roll) list equals the oracle's, order included, in
-    the board-major kernel with per-roll doubles items (K = 4's) and with the
-    six doubles rolls of a row in one item (BGX_REPLY_DBL=1, K = all's), the
-    per-roll kernel and (BGX_MG_TEST_TABLE=1: every root through the per-roll
-    hash-table path) the table cross-check."""
+    the board-major kernel as shipped (a row's six doubles rolls in one item,
+    the last 12/64 of the rows with one item per doubles roll), with every row's
+    doubles in one item (BGX_REPLY_DBL_TAIL=0), with per-roll doubles items only
+    (BGX_REPLY_DBL=0), the per-roll kernel and (BGX_MG_TEST_TABLE=1: every root
+    through the per-roll hash-table path) the table cross-check."""
     monkeypatch.setenv("BGX_REPLY_BM", bm)
     monkeypatch.setenv("BGX_REPLY_DBL", dbl)
+    monkeypatch.setenv("BGX_REPLY_DBL_TAIL", tail)
     monkeypatch.setenv("BGX_MG_TEST_TABLE", table)
     monkeypatch.setenv("BGX_MG_FEW", "0")   # the pool / reply kernels (the engine's large launches)
     boards, opp = _positions()
@@ -65,8 +68,10 @@ def test_reply_moves_vs_oracle(bm, table, dbl, monkeypatch):
 
 def test_reply_kernels_agree_on_engine_records(weights_seed0, monkeypatch):
     """Engine 2-ply K=4 and K=all: the records of a run do not depend on the
-    reply kernel (board-major -- with per-roll doubles items at K = 4 and the
-    board-major doubles at K = all -- vs per-roll)."""
+    reply kernel (board-major, as shipped, vs per-roll). The two kernels
+    reserve their output rows differently, so their gap rows (reserved, never
+    written, still evaluated by the MLP) differ, but the rows holding records,
+    value_rows - gap_rows, are the same count."""
     from bgx import Engine
     from test_gpu_engine import _by_episode, _collect, _same_runs
 
@@ -75,8 +80,12 @@ def test_reply_kernels_agree_on_engine_records(weights_seed0, monkeypatch):
         e = Engine(lanes=320 if k_top == 4 else 48, seed=13, ply=2, k_top=k_top)
         e.set_weights(weights_seed0, temperature=1.5, version=1)
         out = _by_episode(*_collect(e, 160 if k_top == 4 else 120, chunk=40))   # games end from ~50 steps
+        st = e.stats()
         e.close()
-        return out
+        assert 0 <= st["gap_rows"] < st["value_rows"] // 2, st
+        return out, st["value_rows"] - st["gap_rows"]
 
     for k_top in (4, 0):
-        _same_runs(run("1", k_top), run("0", k_top))
+        (a, ra), (b, rb) = run("1", k_top), run("0", k_top)
+        _same_runs(a, b)
+        assert ra == rb, (k_top, ra, rb)

@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 5: board-major doubles with a 12/64 per-roll tail as the default reply
+# launch (K=4 and K=all) + the gap-row stat: 2-ply GPU tests, then the legs
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r5n; mkdir -p $O
+echo "[1] 2-ply tests"
+timeout -k 10 900 python -u -m pytest tests/test_gpu_reply.py tests/test_gpu_engine.py tests/test_gpu_replay.py tests/test_gpu_scale.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+echo "[2] legs"
+K4="--ply 2 --steps 100 --warmup 20 --kall-steps 0 --config1-steps 0 --two-ply-steps 0 --no-cpu-baseline --timing-steps 50"
+KA="--ply 2 --k-top 0 --steps 20 --warmup 5 --kall-steps 0 --config1-steps 0 --two-ply-steps 0 --no-cpu-baseline --timing-steps 10"
+for rep in 1 2; do
+  timeout -k 10 180 python bench.py $K4 > $O/k4_new_$rep.json 2> $O/e.err || { tail -5 $O/e.err; exit 1; }
+  BGX_REPLY_DBL=0 timeout -k 10 180 python bench.py $K4 > $O/k4_roll_$rep.json 2> $O/e.err || { tail -5 $O/e.err; exit 1; }
+  timeout -k 10 180 python bench.py $KA > $O/ka_new_$rep.json 2> $O/e.err || { tail -5 $O/e.err; exit 1; }
+done
+python tools/ab_vals.py $O/k4_*.json $O/ka_*.json
+for f in $O/k4_*.json $O/ka_*.json; do python tools/ab_line.py $(basename $f .json) $f; python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('  gap_rows_frac', d.get('gap_rows_frac'), 'mlp frac', d['roofline']['frac'])" $f; done
