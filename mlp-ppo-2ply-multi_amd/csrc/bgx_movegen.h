@@ -527,7 +527,7 @@ BGX_DEV void cursor_new_chunk(FlatCursor& fc, int base, int n, int grab) {
 // -1: the flat buffer is full (flagged). A request the chunk cannot hold
 // locks the span (bit 31 of its end), refills it with a global reservation
 // sized by the workgroup's progress -- rows per item so far x (items not yet
-// claimed + half the items in flight), between max(n, 64) and 8 x flat_chunk,
+// claimed + a quarter of the items in flight), between max(n, 64) and 8 x flat_chunk,
 // so the chunks shrink as the workgroup's items run out -- and unlocks it;
 // requests that meet the lock wait for the new chunk (one refill at a time:
 // concurrent refills each kept a chunk, 16 per workgroup at a launch's start).
@@ -574,7 +574,7 @@ BGX_DEV int wg_take(const MovegenArgs& a, int n, FlatCursor& fc) {
             // prior: ~107 records per item at K = 4 (8,192 lanes, 12/64 per-roll tail)
             const float per_item = used ? (float)used / (float)(2 * done + flight + 1) * 2.0f : 128.0f;
             const int cap = 8 * a.flat_chunk;
-            const float want_f = per_item * (float)(2 * (items - claimed) + flight + 1) * 0.5f;
+            const float want_f = per_item * ((float)(items - claimed) + 0.25f * (float)flight + 0.5f);
             int want = want_f > (float)cap ? cap : (int)want_f;
             if (want < 64) want = 64;
             const int grab = n > want ? n : want;
