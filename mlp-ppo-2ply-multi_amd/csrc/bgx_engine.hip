@@ -217,7 +217,10 @@ BGX_DEV bool small_double(int j) {   // DICE_ROLLS index 0 = 1-1, 6 = 2-2, 11 = 
 // consecutive rolls of one candidate (a 1-1 with hundreds of replies beside
 // fifteen rolls of a dozen). sample_k > 0: the reference-sampled mode above,
 // keyed by skey and the step salt *salt_dev (null: 0).
-constexpr int T5_GL = 4;
+#ifndef BGX_T5_GL
+#define BGX_T5_GL 4   // lanes per job (A/B builds: 2, 4, 8)
+#endif
+constexpr int T5_GL = BGX_T5_GL;
 constexpr int T5_B = 8;    // loads in flight per lane
 __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
                                                    const int32_t* __restrict__ job_off,
@@ -294,8 +297,8 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
             // the group's largest head (xor-shuffle max over the 4 lanes); the
             // lowest lane holding it pops (ties: lower lane first)
             float mx = t[0];
-            mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+#pragma unroll
+            for (int o = 1; o < T5_GL; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
             const uint32_t grp = (uint32_t)(ballot(t[0] == mx) >> (T5_GL * q)) & ((1u << T5_GL) - 1u);
             const int who = __ffs(grp) - 1;
             if (r < m) s = r ? s + mx : mx;
@@ -478,7 +481,8 @@ extern "C" hipError_t bgx_launch_top5(const float* V, const int32_t* job_off, co
                                       const unsigned long long* salt_dev, unsigned long long* rec_acc,
                                       hipStream_t stream) {
     if (max_jobs <= 0) return hipSuccess;
-    int blocks = (max_jobs + 4 * 16 - 1) / (4 * 16);   // 16 jobs per wave, 4 waves per block
+    constexpr int jw = 64 / bgx::T5_GL;                 // jobs per wave iteration, 4 waves per block
+    int blocks = (max_jobs + 4 * jw - 1) / (4 * jw);
     if (blocks > bgx::T5_WAVES / 4) blocks = bgx::T5_WAVES / 4;   // 8 waves per SIMD on 256 CUs, then loop
     hipLaunchKernelGGL(bgx::top5_kernel, dim3(blocks), dim3(256), 0, stream, V, job_off, job_cnt, n_jobs,
                        n_units_dev, jobs_per_unit, max_jobs, out, sample_k, skey, salt_dev, rec_acc);
