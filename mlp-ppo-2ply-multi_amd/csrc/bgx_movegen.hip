@@ -60,7 +60,7 @@ namespace bgx {
 #define BGX_BND 2          // 1 = the per-roll-round board_nd_records (A/B builds)
 #endif
 #ifndef BGX_REPLY_DBL_TAIL
-#define BGX_REPLY_DBL_TAIL 12   // board-major doubles launch: 64ths of the rows left in per-roll items
+#define BGX_REPLY_DBL_TAIL 4   // board-major doubles launch: 64ths of the rows left in per-roll items
 #endif
 #ifndef BGX_REPLY_WG
 #define BGX_REPLY_WG 1   // A/B builds: 0 = the reply launch's waves reserve rows in per-wave chunks
@@ -627,10 +627,12 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
             // the doubles rolls of a row: one item (board_dbl_emit), except for the
             // last BGX_REPLY_DBL_TAIL / 64 of the rows, whose six rolls are six
             // items, so a workgroup ends on short items. K = 4 at 8,192 lanes (32,768
-            // rows over 512 workgroups): 1.590 ms per step with per-roll items only,
-            // 1.667 with none of them, 1.532-1.536 with 10-24 / 64; K = all: within
-            // noise (7.95-7.99 ms; tools/runs/r5_l.sh, r5_m.sh). BGX_REPLY_DBL=0:
-            // per-roll doubles items only (tests, A/B).
+            // rows over 512 workgroups), per-wave row chunks: 1.590 ms per step with
+            // per-roll items only, 1.667 with none of them, 1.532-1.536 with 10-24 /
+            // 64 (tools/runs/r5_l.sh, r5_m.sh); with the workgroup row chunks the
+            // best tails are smaller: 2-4 / 64 1.405-1.411 ms, 12 / 64 1.419-1.424
+            // (r5_s.sh, r5_t.sh); K = all within noise (7.69-7.80 ms for 0-12).
+            // BGX_REPLY_DBL=0: per-roll doubles items only (tests, A/B).
             ev = getenv("BGX_REPLY_DBL");
             const bool dbl = !ev || atoi(ev) != 0;
             ev = getenv("BGX_REPLY_DBL_TAIL");

@@ -35,14 +35,15 @@ def _reply_lists(boards, opp):
     return u8, off.cpu().numpy(), cnt.cpu().numpy()
 
 
-@pytest.mark.parametrize("bm,table,dbl,tail", [("1", "0", "1", "12"), ("1", "0", "1", "0"), ("1", "0", "0", "12"),
-                                               ("0", "0", "0", "12"), ("1", "1", "0", "12")])
+@pytest.mark.parametrize("bm,table,dbl,tail", [("1", "0", "1", "4"), ("1", "0", "1", "0"), ("1", "0", "1", "32"),
+                                               ("1", "0", "0", "4"), ("0", "0", "0", "4"), ("1", "1", "0", "4")])
 def test_reply_moves_vs_oracle(bm, table, dbl, tail, monkeypatch):
     """Self-play and random placements (bar 0-2, borne-off checkers, closed
     boards): every (board, roll) list equals the oracle's, order included, in
     the board-major kernel as shipped (a row's six doubles rolls in one item,
-    the last 12/64 of the rows with one item per doubles roll), with every row's
-    doubles in one item (BGX_REPLY_DBL_TAIL=0), with per-roll doubles items only
+    the last 4/64 of the rows with one item per doubles roll), with every row's
+    doubles in one item (BGX_REPLY_DBL_TAIL=0) or half the rows per roll (32),
+    with per-roll doubles items only
     (BGX_REPLY_DBL=0), the per-roll kernel and (BGX_MG_TEST_TABLE=1: every root
     through the per-roll hash-table path) the table cross-check."""
     monkeypatch.setenv("BGX_REPLY_BM", bm)

@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 O=gpurun_out/dblg; mkdir -p $O
 B=$PWD/mlp-ppo-2ply-multi_amd/bgx
 for dbl in 0 1; do
-  T="tests/test_gpu_reply.py::test_reply_moves_vs_oracle[1-0-$dbl-12]"
+  T="tests/test_gpu_reply.py::test_reply_moves_vs_oracle[1-0-$dbl-4]"
   BGX_LIB=$B/libbgx_guard.so timeout -k 10 150 python -u -m pytest "$T" -x -q --timeout 120 --timeout-method thread > $O/t_dbl$dbl.log 2>&1 || { tail -30 $O/t_dbl$dbl.log; exit 1; }
   tail -1 $O/t_dbl$dbl.log
 done
