@@ -629,9 +629,9 @@ extern "C" hipError_t bgx_launch_movegen(const bgx::MovegenArgs* args, hipStream
             // items, so a workgroup ends on short items. K = 4 at 8,192 lanes (32,768
             // rows over 512 workgroups), per-wave row chunks: 1.590 ms per step with
             // per-roll items only, 1.667 with none of them, 1.532-1.536 with 10-24 /
-            // 64 (tools/runs/r5_l.sh, r5_m.sh); with the workgroup row chunks the
+            // 64 (tools/runs/README.md r5_l, r5_m); with the workgroup row chunks the
             // best tails are smaller: 2-4 / 64 1.405-1.411 ms, 12 / 64 1.419-1.424
-            // (r5_s.sh, r5_t.sh); K = all within noise (7.69-7.80 ms for 0-12).
+            // (r5_s, r5_t); K = all within noise (7.69-7.80 ms for 0-12).
             // BGX_REPLY_DBL=0: per-roll doubles items only (tests, A/B).
             ev = getenv("BGX_REPLY_DBL");
             const bool dbl = !ev || atoi(ev) != 0;
