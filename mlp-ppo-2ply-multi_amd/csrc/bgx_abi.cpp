@@ -1387,8 +1387,11 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             b.out_packed = e->reply_rows;
             b.flat_count = e->ctr + C_REPLY;
             b.flat_cap = e->reply_cap;
-            // rows a wave reserves per global atomic (its unused tail is a gap row
-            // block the reply MLP evaluates); BGX_FLAT_CHUNK: A/B
+            // output-row reservations: the reply launch's workgroups take chunks of
+            // up to 8 x flat_chunk rows per global atomic (bgx_movegen.h wg_take),
+            // the per-roll pool kernel's waves chunks of up to flat_chunk; a
+            // chunk's unwritten tail is gap rows the reply MLP evaluates
+            // (bgx_stats.gap_rows). BGX_FLAT_CHUNK: A/B
             static const int chunk = [] {
                 const char* v = getenv("BGX_FLAT_CHUNK");
                 return v && atoi(v) >= 64 ? atoi(v) : 512;
