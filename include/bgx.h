@@ -325,7 +325,9 @@ int bgx_ipc_close(void* d_ptr, uint64_t offset);
  * job i * 21 + r's records are rows d_off[j] .. d_off[j] + d_cnt[j] - 1
  * (other rows are unused). Parity hook for the board-major reply kernel
  * (BGX_REPLY_BM=0 selects the per-(board, roll) kernel); BGX_E_CAPACITY when
- * cap is too small. */
+ * cap is too small. Rows are reserved in chunks per workgroup, so cap needs
+ * slack beyond the records: up to 2,048 rows per workgroup of the launch
+ * (min(512, ceil(7 n / 16)) workgroups; bgx/ops.py reply_moves sizes it). */
 int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, uint32_t* d_out, int cap,
                     int32_t* d_off, int32_t* d_cnt, void* stream);
 

@@ -92,7 +92,9 @@ def reply_moves(boards, opponent, cap: int = 0, stream=None):
     boards, opponent = _u8(boards).view(-1, 52), _u8(opponent).view(-1)
     require_cuda(boards, opponent)
     n = boards.shape[0]
-    cap = cap or n * 21 * 64 + 4096
+    # records (<= 64 per (board, roll) on average, generously) + the unwritten
+    # tail of one row chunk (<= 2,048 rows) per workgroup of the launch (<= 512)
+    cap = cap or n * 21 * 64 + min(512, (n * 7 + 15) // 16) * 2048 + 4096
     out = torch.empty((cap, 8), dtype=torch.int32, device=boards.device)
     off = torch.empty((n * 21,), dtype=torch.int32, device=boards.device)
     cnt = torch.empty((n * 21,), dtype=torch.int32, device=boards.device)
