@@ -127,6 +127,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     eng.set_weights(w, temperature=1.5, version=1)
     gathered = [0, 0]
     harvested = [0, 0]   # this rank's own harvests (episodes, records), every run() of the engine
+    collect_t = [0.0, 0]   # rank 0: seconds inside hg.collect (+ its copies at --collect-copy), batches
     hg = None
     if world > 1 and args.gather in ("host", "device"):
         from bgx import devgather, hostgather
@@ -164,7 +165,14 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
             if hg is not None:      # DMA engines into host shared memory / rank 0's GPU; no collective
                 seq[0] += 1
                 if rank == 0:
-                    for part in hg.collect(seq[0], copy=False):
+                    tc = time.perf_counter()
+                    # --collect-copy: the peers' batches cloned on rank 0's stream, as a GPU
+                    # trainer takes them (devgather.collect synchronises that stream, which
+                    # carries this rank's own persistent launch, before acknowledging)
+                    parts = hg.collect(seq[0], copy=args.collect_copy)
+                    collect_t[0] += time.perf_counter() - tc
+                    collect_t[1] += 1
+                    for part in parts:
                         if part is not None:
                             gathered[0] += part[0].shape[0]
                             gathered[1] += part[1].shape[0]
@@ -206,6 +214,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     run(warmup)
     eng.sync()
     s0 = eng.stats()
+    c0 = list(collect_t)
     barrier(world)
     t0 = time.perf_counter()
     run(steps)          # direct launches, no events in the stream
@@ -213,6 +222,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     el = time.perf_counter() - t0
     s1 = eng.stats()
     d = {k: s1[k] - s0[k] for k in s1}
+    d["collect_s"], d["collect_batches"] = collect_t[0] - c0[0], collect_t[1] - c0[1]   # the timed window's
     tm = d_tm = None
     if timing:
         # per-kernel durations: a second pass of the same workload with HIP
@@ -273,8 +283,10 @@ def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
     fixtures) as `procs` processes, each pinned to its own host core: one
     1-ply round per seed, each process timing its window after a 300-step
     warm-up of whole games (BASELINE.md's plan; median of the per-round
-    aggregates), then one 2-ply K=4 round (no warm-up: at ~30 decisions/s per
-    core it would take ten seconds). Runs before this process touches the GPU."""
+    aggregates), then one 2-ply K=4 round whose 300-step warm-up plays 1-ply
+    decisions (2-ply ones take ~30 ms each on a core) and ends mid-game, so
+    the 2-ply window starts from the self-play position mix, not the
+    openings. Runs before this process touches the GPU."""
     import multiprocessing as mp
     cores = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
     ctx = mp.get_context("spawn")
@@ -299,7 +311,7 @@ def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
             rates.append(sum(r["steps"] for r in rs) / el)
         out["1ply"] = {"rates": rates, "median": float(np.median(rates))}
         if seconds_2ply > 0:
-            rs, el = round_(77, 2, seconds_2ply)
+            rs, el = round_(77, 2, seconds_2ply, warmup=CPU_WARMUP_STEPS)
             out["2ply"] = {"value": sum(r["steps"] for r in rs) / el,
                            "decisions_per_s": sum(r["decisions"] for r in rs) / el, "elapsed": el}
     finally:
@@ -449,6 +461,9 @@ def main():
                     help="2-ply K=all leg (configs[2]: ~21 x C reply boards per decision); 0 = skip")
     ap.add_argument("--config1-steps", type=int, default=300,
                     help="N = 1: configs[1] (4,096 lanes, 1-ply) beside the headline; 0 = skip")
+    ap.add_argument("--config2-steps", type=int, default=100,
+                    help="N = 1: configs[2] (4,096 lanes, 2-ply) beside the headline: K=4 for this many steps, "
+                         "K=all for a fifth of them; 0 = skip")
     ap.add_argument("--cpu-procs", type=int, default=7, help="pinned CPU-port processes (src/main.py:86: 7 workers)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="per 1-ply round (one round per seed)")
     ap.add_argument("--cpu-seeds", type=int, default=5, help="seeds 0..n-1, median reported")
@@ -460,6 +475,9 @@ def main():
                     help="N > 1 episode gather to rank 0: 'host' = DMA-engine copies into host shared memory "
                          "(no kernels, no collective per harvest); 'device' = DMA-engine peer copies into rank 0's "
                          "GPU memory (xGMI, the GPU trainer's input); 'rccl' = RCCL point-to-point over xGMI")
+    ap.add_argument("--collect-copy", action="store_true",
+                    help="N > 1: rank 0 clones each gathered batch on its GPU (devgather.collect(copy=True), the "
+                         "GPU trainer's input) instead of reading the slots in place")
     ap.add_argument("--no-balance", action="store_true",
                     help="fused 1-ply: every lane runs exactly the steps of a call (lockstep) instead of the "
                          "balanced launch (a step(n) call = n x lanes lane-steps, faster workgroups run ahead)")
@@ -487,7 +505,9 @@ def main():
             cpu["two_ply_k4"] = {"value": r["2ply"]["value"], "unit": "env_steps/s",
                                  "decisions_per_s": r["2ply"]["decisions_per_s"],
                                  "sample": f"{args.cpu_procs} pinned processes x {r['2ply']['elapsed']:.1f} s of "
-                                           "2-ply K=4 self-play (exact mode, fp32) with the same CPU port; the "
+                                           f"2-ply K=4 self-play (exact mode, fp32) with the same CPU port, each "
+                                           f"after a {CPU_WARMUP_STEPS}-step warm-up of 1-ply decisions that ends "
+                                           "mid-game (the window starts from the self-play position mix); the "
                                            "reference's Python 2-ply takes 205 ms per decision (BASELINE.md)"}
 
     world, rank, local = init_dist()
@@ -514,6 +534,9 @@ def main():
                 "seed": args.seed if seed is None else seed}
         if world > 1:
             out_["gathered_episodes"], out_["gathered_records"] = gathered_
+            if rank == 0 and d_.get("collect_batches"):   # rank 0's time in collect() per batch vs the interval
+                out_["collect_ms_per_batch"] = d_["collect_s"] / d_["collect_batches"] * 1e3
+                out_["harvest_interval_ms"] = el_ / d_["collect_batches"] * 1e3
             # what each rank harvested (all of the engine's runs, as the gather counts)
             out_["harvested_episodes_per_rank"] = [int(x) for x in all_ranks(harvested_[0], world)]
             out_["harvested_records_per_rank"] = [int(x) for x in all_ranks(harvested_[1], world)]
@@ -569,6 +592,17 @@ def main():
                  leg(1, 4, 4096, args.config1_steps, 100, min(args.config1_steps, args.timing_steps), "1ply"))
         extra["configs1_4096_lanes"] = {k: c1[k] for k in ("value", "unit", "steps", "ms_per_step", "roofline")
                                         + (("protocol",) if proto else ())}
+    if args.ply == 1 and world == 1 and args.config2_steps > 0 and args.lanes != 4096:
+        # configs[2]: 4,096 lanes, 2-ply on one MI355X (its "~21^2 next-boards/step" is K=all; K=4 is the
+        # reference's two_ply.py:67-70 default), both legs at that lane count
+        keys = ("value", "unit", "steps", "ms_per_step", "decisions_per_s", "gap_rows_frac", "roofline", "kernels")
+        c2 = {}
+        for name, k_top, n, wu in (("2ply_k4", 4, args.config2_steps, 20),
+                                   ("2ply_kall", 0, max(5, args.config2_steps // 5), 5)):
+            r, _ = (protocol(2, k_top, 4096, wu, min(args.timing_steps, 50 if k_top else 10), name, n) if proto else
+                    leg(2, k_top, 4096, n, wu, min(n, args.timing_steps, 50 if k_top else 10), name))
+            c2[name.replace("2ply_", "two_ply_")] = {k: r[k] for k in keys + (("protocol",) if proto else ())}
+        extra["configs2_4096_lanes"] = c2
 
     if rank == 0:
         line = {
@@ -604,8 +638,9 @@ def main():
         }
         if world > 1:
             for k in ("gathered_episodes", "gathered_records", "harvested_episodes_per_rank",
-                      "harvested_records_per_rank"):
-                line[k] = head[k]
+                      "harvested_records_per_rank", "collect_ms_per_batch", "harvest_interval_ms"):
+                if k in head:
+                    line[k] = head[k]
         line.update(extra)
         print(json.dumps(line))
     if world > 1:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define BGX_ABI_VERSION 9
+#define BGX_ABI_VERSION 10
 
 #define BGX_OK 0
 #define BGX_E_ARG -1        /* invalid argument */
@@ -250,6 +250,29 @@ typedef struct bgx_stats {
 } bgx_stats;
 int bgx_get_stats(bgx_engine* e, bgx_stats* out);  /* synchronizes */
 
+/* Test hook: copy one of the phased engine's per-step device buffers to host
+ * (synchronizes the engine stream), so a parity test can compare what a
+ * bgx_step computed at the benchmarked shape with the oracle. After a step:
+ * the candidates of that step (their rows, per-lane offset / count, V) and,
+ * at ply 2, the top-k choice and the per-(candidate, roll) top-5 reply means
+ * that two_ply.py:93-150 averages into W (job (candidate row - L) * 21 + roll
+ * at K = all, (4 * lane + k) * 21 + roll at K = 4; DICE_ROLLS order,
+ * two_ply.py:10-32). Before a step: the lanes' boards, players and dice.
+ * h_out = null returns the size in *needed only. The fused 1-ply engine keeps
+ * its candidates in workgroup-private buffers: only PLAYER / DICE there. */
+enum {
+    BGX_PEEK_LANE_ROWS = 0,   /* u32 [L][8] packed lane boards */
+    BGX_PEEK_PLAYER = 1,      /* u8 [L] player to move */
+    BGX_PEEK_DICE = 2,        /* u8 [L][2] the roll to play */
+    BGX_PEEK_CAND_OFF = 3,    /* i32 [L] first candidate row (after row L) */
+    BGX_PEEK_CAND_CNT = 4,    /* i32 [L] candidates (all, before the max_legal cap) */
+    BGX_PEEK_CAND_ROWS = 5,   /* u32 [cand_cap][8] packed candidate boards */
+    BGX_PEEK_VALUES = 6,      /* f32 [L + cand_cap] V of the lane rows, then of the candidates */
+    BGX_PEEK_SEL = 7,         /* i32 [L][4] K = 4: the chosen candidate rows (-1: fewer than 4 moves) */
+    BGX_PEEK_JOB_VAL = 8      /* f32 [jobs] top-5 mean of the replies per (candidate, roll) */
+};
+int bgx_engine_peek(bgx_engine* e, int buf, void* h_out, uint64_t bytes, uint64_t* needed);
+
 /* Kernel timing (HIP events on the engine stream, recorded per bgx_step while
  * enabled): total milliseconds and launch counts of the movegen and MLP
  * kernels since the last reset. A fused engine (bgx_config.fused, 1-ply)
@@ -326,8 +349,10 @@ int bgx_ipc_close(void* d_ptr, uint64_t offset);
  * (other rows are unused). Parity hook for the board-major reply kernel
  * (BGX_REPLY_BM=0 selects the per-(board, roll) kernel); BGX_E_CAPACITY when
  * cap is too small. Rows are reserved in chunks per workgroup, so cap needs
- * slack beyond the records: up to 2,048 rows per workgroup of the launch
- * (min(512, ceil(7 n / 16)) workgroups; bgx/ops.py reply_moves sizes it). */
+ * slack beyond the records: per workgroup of the launch (min(2 x CUs,
+ * ceil(7 n / 16)) workgroups) its last chunk's unwritten tail (<= 2,048 rows)
+ * and its waves' kept remainders (each smaller than one job's records);
+ * bgx/ops.py reply_moves allows 4,096 rows per workgroup. */
 int bgx_reply_moves(const uint8_t* d_boards, const uint8_t* d_opponent, int n, uint32_t* d_out, int cap,
                     int32_t* d_off, int32_t* d_cnt, void* stream);
 

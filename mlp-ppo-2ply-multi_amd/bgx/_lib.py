@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("BGX_LIB", os.path.join(_HERE, "libbgx.so"))
 c_int, c_float, c_double, c_u64, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                              ctypes.c_uint64, ctypes.c_void_p)
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class BgxError(RuntimeError):
@@ -76,6 +76,7 @@ SIGNATURES = {
     "bgx_harvest_enqueue": (c_int, [c_void_p, ctypes.POINTER(c_int), c_void_p]),
     "bgx_harvest_fetch": (c_int, [c_void_p, c_int, ctypes.POINTER(HarvestInfo)]),
     "bgx_get_stats": (c_int, [c_void_p, ctypes.POINTER(Stats)]),
+    "bgx_engine_peek": (c_int, [c_void_p, c_int, c_void_p, c_u64, ctypes.POINTER(c_u64)]),
     "bgx_set_timing": (c_int, [c_void_p, c_int]),
     "bgx_get_timing": (c_int, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int),
                                ctypes.POINTER(c_double), ctypes.POINTER(c_int)]),

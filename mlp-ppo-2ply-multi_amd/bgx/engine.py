@@ -142,6 +142,23 @@ class Engine:
         check(lib().bgx_get_stats(self._h, ctypes.byref(s)), "bgx_get_stats")
         return {k: int(getattr(s, k)) for k, _ in Stats._fields_}
 
+    PEEK = {"lane_rows": (0, "<u4", 8), "player": (1, "u1", 1), "dice": (2, "u1", 2), "cand_off": (3, "<i4", 1),
+            "cand_cnt": (4, "<i4", 1), "cand_rows": (5, "<u4", 8), "values": (6, "<f4", 1), "sel": (7, "<i4", 4),
+            "job_val": (8, "<f4", 21)}
+
+    def peek(self, name):
+        """Test hook (bgx_engine_peek): a host copy of one of the phased
+        engine's per-step buffers, e.g. the candidates and the per-(candidate,
+        roll) top-5 reply means of the last 2-ply step (include/bgx.h)."""
+        import numpy as np
+        buf, dt, width = self.PEEK[name]
+        n = ctypes.c_uint64(0)
+        check(lib().bgx_engine_peek(self._h, buf, None, 0, ctypes.byref(n)), "bgx_engine_peek")
+        out = np.empty(int(n.value) // np.dtype(dt).itemsize, dtype=dt)
+        check(lib().bgx_engine_peek(self._h, buf, out.ctypes.data_as(ctypes.c_void_p), int(n.value), None),
+              "bgx_engine_peek")
+        return out.reshape(-1, width) if width > 1 else out
+
     def set_timing(self, enabled=True):
         check(lib().bgx_set_timing(self._h, 1 if enabled else 0), "bgx_set_timing")
 

@@ -56,14 +56,18 @@ class Staging:
         check(lib().bgx_dma_copy_d2h(self.addr + hb, h.records.data_ptr(), rb, self.device, ctypes.byref(t2)),
               "bgx_dma_copy_d2h")
         from ._lib import BgxError
+        tickets = [t1.value, t2.value]
         try:
-            check(lib().bgx_dma_wait(t1.value, timeout_ms), "bgx_dma_wait")
-            check(lib().bgx_dma_wait(t2.value, timeout_ms), "bgx_dma_wait")
+            while tickets:
+                check(lib().bgx_dma_wait(tickets[0], timeout_ms), "bgx_dma_wait")
+                tickets.pop(0)   # released by the successful wait
         except BgxError:
             # a copy still in flight owns the staging buffer and the harvest's
-            # arrays: keep both for the life of the process, refuse further copies
+            # arrays: keep both for the life of the process, with the tickets not
+            # yet waited for (each still holds its completion signal; a later
+            # bgx_dma_wait on one of them releases it), and refuse further copies
             from .hostgather import STUCK_COPIES
-            STUCK_COPIES.append((self.mm, self.buf, h))
+            STUCK_COPIES.append((self.mm, self.buf, h, tuple(tickets)))
             self.mm = self.buf = self.addr = None
             self.size = 0
             self.broken = True

@@ -92,9 +92,13 @@ def reply_moves(boards, opponent, cap: int = 0, stream=None):
     boards, opponent = _u8(boards).view(-1, 52), _u8(opponent).view(-1)
     require_cuda(boards, opponent)
     n = boards.shape[0]
-    # records (<= 64 per (board, roll) on average, generously) + the unwritten
-    # tail of one row chunk (<= 2,048 rows) per workgroup of the launch (<= 512)
-    cap = cap or n * 21 * 64 + min(512, (n * 7 + 15) // 16) * 2048 + 4096
+    # records (<= 64 per (board, roll) on average, generously) + per workgroup
+    # of the launch (two per CU, at most ceil(7 n / 16): bgx_launch_movegen) two
+    # row chunks' worth (2 x 2,048 rows: its last chunk's tail and its waves'
+    # kept remainders, each smaller than one request); running out is an error
+    # (BGX_E_CAPACITY), never a silent truncation
+    n_cu = torch.cuda.get_device_properties(boards.device).multi_processor_count
+    cap = cap or n * 21 * 64 + min(2 * n_cu, (n * 7 + 15) // 16) * 2 * 2048 + 4096
     out = torch.empty((cap, 8), dtype=torch.int32, device=boards.device)
     off = torch.empty((n * 21,), dtype=torch.int32, device=boards.device)
     cnt = torch.empty((n * 21,), dtype=torch.int32, device=boards.device)

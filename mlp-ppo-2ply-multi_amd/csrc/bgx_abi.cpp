@@ -1096,6 +1096,18 @@ int bgx_engine_destroy(bgx_engine* e) {
     });
 }
 
+// Rows per reply-launch reservation unit (MovegenArgs::flat_chunk): 512 by
+// default, BGX_FLAT_CHUNK in [64, 1024] for A/B runs (the engine's reply_cap
+// slack is sized from it, so it is bounded above too).
+static int reply_flat_chunk() {
+    static const int chunk = [] {
+        const char* v = getenv("BGX_FLAT_CHUNK");
+        const int c = v ? atoi(v) : 512;
+        return c < 64 ? 512 : (c > 1024 ? 1024 : c);
+    }();
+    return chunk;
+}
+
 int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
     return guarded("bgx_engine_create", [&]() -> int {
         if (!cfg || !out) return fail(BGX_E_ARG, "bgx_engine_create: null pointer");
@@ -1194,8 +1206,14 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             const int per_lane = cfg->reply_per_lane > 0 ? cfg->reply_per_lane : (cfg->k_top == 4 ? 4096 : 16384);
             int n_cu = 256;
             if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) n_cu = 256;
-            // + the slack of one partly used 512-row reservation per resident movegen wave (<= 32 / CU)
-            e->reply_cap = L * per_lane + n_cu * 32 * 512;
+            // + slack for the rows reserved but left unwritten: the reply launch
+            // runs two workgroups per CU (bgx_launch_movegen), each ending with at
+            // most one workgroup chunk (<= 8 x flat_chunk rows) and its waves'
+            // kept remainders (tails of replaced chunks, each smaller than the
+            // request that replaced it); two chunks' worth per workgroup covers
+            // both (measured gap rows: 2-3 % of a K = 4 step's rows, DESIGN.md
+            // section 4). Running out is flagged (BGX_E_CAPACITY), not silent.
+            e->reply_cap = L * per_lane + n_cu * 2 * 2 * 8 * reply_flat_chunk();
             ALLOC(e->sel, 4 * L);
             ALLOC(e->sel_rows, (size_t)4 * L * 8);
             ALLOC(e->reply_rows, (size_t)e->reply_cap * 8);
@@ -1391,12 +1409,8 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             // up to 8 x flat_chunk rows per global atomic (bgx_movegen.h wg_take),
             // the per-roll pool kernel's waves chunks of up to flat_chunk; a
             // chunk's unwritten tail is gap rows the reply MLP evaluates
-            // (bgx_stats.gap_rows). BGX_FLAT_CHUNK: A/B
-            static const int chunk = [] {
-                const char* v = getenv("BGX_FLAT_CHUNK");
-                return v && atoi(v) >= 64 ? atoi(v) : 512;
-            }();
-            b.flat_chunk = chunk;
+            // (bgx_stats.gap_rows)
+            b.flat_chunk = reply_flat_chunk();
             b.job_off = e->job_off;
             b.job_cnt = e->job_cnt;
             mg_common(e, b);
@@ -1659,7 +1673,41 @@ int bgx_get_stats(bgx_engine* e, bgx_stats* out) {
         out->value_rows = st[3];
         out->movegen_jobs = st[4];
         out->fallback_jobs = st[5];
-        out->gap_rows = st[6] - st[7];   // 2-ply reply rows reserved minus the records written into them
+        // 2-ply reply rows reserved minus the records written into them; a step
+        // stopped between the top-5 launch (st[7]) and the step kernel (st[6])
+        // would make the difference negative, so clamp at zero
+        out->gap_rows = st[6] > st[7] ? st[6] - st[7] : 0;
+        return BGX_OK;
+    });
+}
+
+int bgx_engine_peek(bgx_engine* e, int buf, void* h_out, uint64_t bytes, uint64_t* needed) {
+    return guarded("bgx_engine_peek", [&]() -> int {
+        if (!e) return fail(BGX_E_ARG, "bgx_engine_peek: null engine");
+        const size_t L = (size_t)e->cfg.lanes;
+        const void* src = nullptr;
+        size_t n = 0;
+        switch (buf) {
+        case BGX_PEEK_LANE_ROWS: src = e->rows; n = L * 8 * 4; break;
+        case BGX_PEEK_PLAYER: src = e->d.player; n = L; break;
+        case BGX_PEEK_DICE: src = e->d.dice; n = 2 * L; break;
+        case BGX_PEEK_CAND_OFF: src = e->cand_off; n = L * 4; break;
+        case BGX_PEEK_CAND_CNT: src = e->cand_cnt; n = L * 4; break;
+        case BGX_PEEK_CAND_ROWS: src = e->rows + L * 8; n = (size_t)e->cand_cap * 8 * 4; break;
+        case BGX_PEEK_VALUES: src = e->V; n = (L + (size_t)e->cand_cap) * 4; break;
+        case BGX_PEEK_SEL: src = e->sel; n = e->sel ? 4 * L * 4 : 0; break;
+        case BGX_PEEK_JOB_VAL: src = e->job_val; n = e->job_val ? (size_t)e->jobs_cap * 4 : 0; break;
+        default: return fail(BGX_E_ARG, "bgx_engine_peek: unknown buffer %d", buf);
+        }
+        if (e->fused && buf != BGX_PEEK_PLAYER && buf != BGX_PEEK_DICE)
+            return fail(BGX_E_STATE, "bgx_engine_peek: buffer %d is not kept by the fused engine", buf);
+        if (!src || n == 0) return fail(BGX_E_STATE, "bgx_engine_peek: buffer %d not allocated (ply %d)", buf, e->cfg.ply);
+        if (needed) *needed = n;
+        if (!h_out) return BGX_OK;
+        if (bytes < n) return fail(BGX_E_ARG, "bgx_engine_peek: %llu bytes < %zu", (unsigned long long)bytes, n);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->last) HIP_TRY(hipStreamSynchronize(e->last));
+        HIP_TRY(hipMemcpy(h_out, src, n, hipMemcpyDeviceToHost));
         return BGX_OK;
     });
 }

@@ -15,7 +15,11 @@
 #define BGX_TILE_PRIO_EPI 0   // 1: the priority holds through the epilogue (exp / rcp) too (A/B)
 #endif
 #ifndef BGX_TILE_NOSKIP
-#define BGX_TILE_NOSKIP 1   // 1: mlp_tile4 runs every k-step (straight-line code); 0: zero k-steps skipped (A/B builds)
+#define BGX_TILE_NOSKIP 1   // 1: mlp_tile4 runs every k-step (straight-line code); 0: zero k-steps skipped (A/B builds;
+                            // only the BGX_TILE_PF=0 form has the skip, so NOSKIP=0 needs TILE_PF=0)
+#endif
+#if BGX_TILE_PF && !BGX_TILE_NOSKIP
+#error "BGX_TILE_NOSKIP=0 (zero k-steps skipped) exists only in the BGX_TILE_PF=0 tile; build with -DBGX_TILE_PF=0"
 #endif
 
 namespace bgx {

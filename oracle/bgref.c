@@ -681,7 +681,8 @@ typedef struct {
     long long steps, decisions, episodes;
     int ply;          /* 1: softmax(V/T) over every candidate (worker.py:137-143);
                          2: two_ply.py:44-90 scoring of the top-4 by V, softmax over the four */
-    long long warmup; /* untimed env steps first (whole games, BASELINE.md: a 300-step warm-up) */
+    long long warmup; /* untimed env steps first (a 300-step warm-up): whole games at ply 1; at
+                         ply 2 1-ply decisions, ending mid-game so the 2-ply window starts in the mix */
     double elapsed;   /* the thread's timed window */
 } sp_arg;
 
@@ -767,6 +768,14 @@ static void* sp_thread(void* p) {
         int co[2] = {0, 0}, pg[2] = {0, 0};
         int done = 0, step = 0;
         while (!done && step < 300) {
+            /* 2-ply: the warm-up plays 1-ply decisions (cheap) and ends mid-game,
+               so the timed 2-ply window starts from the self-play position mix */
+            if (warm && a->ply == 2 && steps + step >= a->warmup) {
+                warm = 0;
+                steps = -step;   /* += step at the game's end: the steps after the switch */
+                dec = eps = 0;
+                t0 = now_s();
+            }
             full_t* fm;
             int n = all_moves(board, pl, roll[0], roll[1], &fm);
             if (n > 500) n = 500;
@@ -788,7 +797,7 @@ static void* sp_thread(void* p) {
             int cand[500], m = n;
             double sc[500];
             for (int i = 0; i < n; ++i) { cand[i] = i; sc[i] = v[i + 1]; }
-            if (a->ply == 2 && n >= 4) {
+            if (a->ply == 2 && n >= 4 && !warm) {
                 for (int c = 0; c < 4; ++c) {   /* top-4 by V, ties to the lower index */
                     int best = c;
                     for (int i = c + 1; i < n; ++i)

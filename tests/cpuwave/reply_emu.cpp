@@ -56,7 +56,11 @@ int main(int argc, char** argv) {
     b.ws_words_per_wave = (size_t)5 * ws_slots;
     b.err_flags = ctr.data() + 3;
     if (bgx_launch_movegen(&b, nullptr) != hipSuccess) return 3;
-    printf("{\"roots\": %d, \"rows\": %u, \"tier2_jobs\": %u, \"flags\": %u}\n", n, ctr[0], ctr[2], ctr[3]);
+    // job_off / job_cnt start poisoned (-7): every job of the launch must write both
+    int unwritten = 0;
+    for (int j = 0; j < n_jobs; ++j) unwritten += off[j] == -7 || cnt[j] == -7;
+    printf("{\"roots\": %d, \"rows\": %u, \"tier2_jobs\": %u, \"flags\": %u, \"unwritten_jobs\": %d}\n", n, ctr[0],
+           ctr[2], ctr[3], unwritten);
     FILE* f = fopen(argv[3], "wb");
     if (!f) return 2;
     for (int j = 0; j < n_jobs; ++j) {
@@ -65,5 +69,5 @@ int main(int argc, char** argv) {
             fwrite(out.data() + (size_t)off[j] * 8, 4, (size_t)cnt[j] * 8, f);
     }
     fclose(f);
-    return ctr[3] ? 4 : 0;
+    return ctr[3] ? 4 : (unwritten ? 5 : 0);
 }

@@ -44,7 +44,7 @@ def test_ctypes_table_covers_header(built):
 def test_loads_without_gpu_and_reports_version(built):
     import bgx
     L = bgx.lib()
-    assert L.bgx_abi_version() == 9
+    assert L.bgx_abi_version() == 10
     assert L.bgx_last_error() is not None
 
 

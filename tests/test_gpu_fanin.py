@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--gpus", "8", "--lanes", "1024", "--steps", "60", "--warmup", "10", "--desync-steps", "60",
         "--harvest-every", "30", "--two-ply-steps", "0", "--kall-steps", "0", "--config1-steps", "0",
-        "--timing-steps", "0", "--gather", "host"]
+        "--timing-steps", "0"]
 
 
 def _env(**extra):
@@ -32,9 +32,16 @@ def _env(**extra):
     return env
 
 
-def test_bench_world8_host_fanin_on_one_gpu():
-    r = subprocess.run([sys.executable, "bench.py", *ARGS], cwd=REPO, env=_env(), capture_output=True, text=True,
-                       timeout=420)
+@pytest.mark.parametrize("gather", ["host", "device-copy"])
+def test_bench_world8_fanin_on_one_gpu(gather):
+    """host: the default hand-off. device-copy: the device gather (slots in rank
+    0's GPU memory, opened by the 7 peers over IPC, SDMA peer copies;
+    bgx/devgather.py), rank 0 cloning every batch on its own stream as the GPU
+    trainer takes it (collect(copy=True)); the JSON line then reports rank 0's
+    time inside collect() per batch beside the harvest interval."""
+    extra = ["--gather", "host"] if gather == "host" else ["--gather", "device", "--collect-copy"]
+    r = subprocess.run([sys.executable, "bench.py", *ARGS, *extra], cwd=REPO, env=_env(), capture_output=True,
+                       text=True, timeout=420)
     assert r.returncode == 0, r.stderr[-4000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 8 and line["world_size"] == 8
@@ -43,11 +50,15 @@ def test_bench_world8_host_fanin_on_one_gpu():
     assert len(eps) == 8 and min(eps) > 0
     assert line["gathered_episodes"] == sum(eps), (line["gathered_episodes"], eps)
     assert line["gathered_records"] == sum(recs), (line["gathered_records"], recs)
+    assert line["collect_ms_per_batch"] >= 0 and line["harvest_interval_ms"] > 0
+    print(f"[fanin {gather}] collect {line['collect_ms_per_batch']:.3f} ms per batch, harvest interval "
+          f"{line['harvest_interval_ms']:.3f} ms, {line['value'] / 1e6:.2f} M env steps/s")
 
 
 def test_bench_world8_failed_rank_ends_the_run():
     t0 = time.monotonic()
-    r = subprocess.run([sys.executable, "bench.py", *ARGS], cwd=REPO, env=_env(BGX_BENCH_FAIL_RANK="5"),
+    r = subprocess.run([sys.executable, "bench.py", *ARGS, "--gather", "host"], cwd=REPO,
+                       env=_env(BGX_BENCH_FAIL_RANK="5"),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "BGX_BENCH_FAIL_RANK" in r.stderr

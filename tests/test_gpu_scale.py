@@ -170,6 +170,136 @@ def test_kall_4096_lanes_greedy_is_oracle_argmax(weights_seed0):
     assert len(res) == 2000
 
 
+# two_ply.py:10-32 DICE_ROLLS order; a double has probability 1/36, the others 2/36
+ROLLS = [(a, b) for a in range(1, 7) for b in range(a, 7)]
+ROLL_P = np.array([1.0 / 36 if a == b else 2.0 / 36 for a, b in ROLLS])
+
+
+def _unpack(w):
+    """packed rows uint32 [n, 8] -> uint8 [n, 52] (bgx_device.h packed_to_u8)"""
+    w = np.asarray(w, np.uint32).reshape(-1, 8)
+    out = np.zeros((w.shape[0], 52), np.uint8)
+    for k in range(6):
+        for q in range(8):
+            out[:, 8 * k + q] = (w[:, k] >> (4 * q)) & 15
+    for i in range(4):
+        out[:, 48 + i] = (w[:, 6] >> (4 * i)) & 15
+    return out
+
+
+def _peek_step(e):
+    """One engine step between two peeks: the lanes' positions before it, and
+    the candidates, V and per-(candidate, roll) top-5 reply means it computed."""
+    before = {k: e.peek(k) for k in ("lane_rows", "player", "dice")}
+    e.step(1)
+    after = {k: e.peek(k) for k in ("cand_off", "cand_cnt", "cand_rows", "values", "job_val")}
+    if e.cfg.k_top == 4:
+        after["sel"] = e.peek("sel")
+    return before, after
+
+
+def _check_lane_w(w, lanes, before, after, i):
+    """Lane i of a peeked 2-ply step against the oracle: its candidate boards
+    in the reference's order (bit-exact), V(candidate) within 1e-5, and W of
+    every candidate the step scored (K = all: every one; K = 4: the top 4 by V)
+    as the DICE_ROLLS-weighted top-5 means, within 1e-5 of the oracle's
+    two_ply_response (two_ply.py:93-150). Returns the number of W compared."""
+    board = _unpack(before["lane_rows"][i])[0]
+    mover = int(before["player"][i])
+    d0, d1 = (int(x) for x in before["dice"][i])
+    cnt, res, _ = orc.movegen(board, mover, d0, d1)
+    assert int(after["cand_cnt"][i]) == cnt, (i, int(after["cand_cnt"][i]), cnt)
+    m = min(cnt, 500)
+    if m == 0:
+        return 0
+    off = int(after["cand_off"][i])
+    got = _unpack(after["cand_rows"][off:off + m])
+    assert np.array_equal(got, res[:m]), i
+    v = orc.value(w, orc.encode_many(res[:m], [mover] * m))
+    gv = after["values"][lanes + off:lanes + off + m].astype(np.float64)
+    assert np.abs(gv - v).max() < V_TOL, (i, float(np.abs(gv - v).max()))
+    if "sel" in after:
+        sel = after["sel"][i]
+        if sel[0] < 0:
+            assert m < 4
+            return 0
+        cand = [int(s) - lanes - off for s in sel]
+        rest = np.delete(v, cand)
+        assert len(set(cand)) == 4 and (rest.size == 0 or v[cand].min() >= rest.max() - V_TOL), (i, cand)
+        jv = after["job_val"].reshape(-1, 21)[4 * i:4 * i + 4]
+    else:
+        cand = list(range(m))
+        jv = after["job_val"].reshape(-1, 21)[off:off + m]
+    n = 0
+    for c, row in zip(cand, jv):
+        assert 0 <= c < m
+        W_eng = float(np.dot(row.astype(np.float64), ROLL_P))
+        W_orc = orc.two_ply_response(w, res[c], 1 - mover)
+        assert abs(W_eng - W_orc) < V_TOL, (i, c, W_eng, W_orc)
+        n += 1
+    return n
+
+
+def test_kall_8192_lanes_w_and_greedy_argmax(weights_seed0):
+    """2-ply K = all at the bench's 8,192-lane shape (bench.py's K = all leg:
+    the same grid, reply row chunks and refills), greedy. (1) One step between
+    two peeks (bgx_engine_peek): for >= 500 lanes the step's candidate boards
+    equal the oracle's movegen, their V is within 1e-5, and W of every
+    candidate -- the DICE_ROLLS-weighted means of the engine's per-(candidate,
+    roll) top-5 reply values -- is within 1e-5 of the oracle's
+    two_ply_response (two_ply.py:93-150). (2) >= 2,000 sampled decisions of
+    the following steps equal the oracle's argmax of 1.0 * V - 0.9 * W
+    (two_ply.py:44-90)."""
+    from bgx.episodes import decode_records
+    lanes = 8192
+    e = _engine(weights_seed0, lanes=lanes, seed=37, ply=2, k_top=0, greedy=True)
+    e.step(100)                 # lanes spread over their games
+    e.harvest()
+    before, after = _peek_step(e)
+    e.step(60)
+    h = e.harvest()
+    hdr = h.headers.cpu().numpy().view(np.uint32)
+    d = decode_records(hdr, h.records)
+    e.close()
+    rng = np.random.default_rng(13)
+    movers = [i for i in rng.permutation(lanes) if int(after["cand_cnt"][i]) > 0][:600]
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:   # ctypes drops the GIL
+        nw = list(ex.map(lambda i: _check_lane_w(weights_seed0, lanes, before, after, i), movers))
+    assert len(movers) == 600 and sum(nw) >= 5000, (len(movers), sum(nw))
+
+    m = d["action"].shape[0]
+    assert m > 20000
+    ks = rng.choice(m, 2000, replace=False)
+
+    def one(k):
+        s = _kall_scores(weights_seed0, d["before"][k], int(d["mover"][k]), *d["dice"][k])
+        a = int(d["action"][k])
+        return a, float(s[a]), float(s.max()), len(s)
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(one, ks))
+    for k, (a, sa, smax, n) in zip(ks, res):
+        assert 0 <= a < n
+        assert sa >= smax - 2 * V_TOL, (int(k), a, sa, smax)
+
+
+def test_k4_8192_lanes_w(weights_seed0):
+    """2-ply K = 4 at 8,192 lanes (bench.py's K = 4 leg, sampling as the bench
+    runs it): one peeked step, >= 500 lanes with >= 4 moves -- the engine's
+    top 4 by V and each one's W within 1e-5 of the oracle's."""
+    lanes = 8192
+    e = _engine(weights_seed0, lanes=lanes, seed=43, ply=2, k_top=4)
+    e.step(100)
+    e.harvest()
+    before, after = _peek_step(e)
+    e.close()
+    rng = np.random.default_rng(17)
+    movers = [i for i in rng.permutation(lanes) if int(after["cand_cnt"][i]) >= 4][:500]
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        nw = list(ex.map(lambda i: _check_lane_w(weights_seed0, lanes, before, after, i), movers))
+    assert len(movers) == 500 and sum(nw) == 2000
+
+
 @pytest.mark.parametrize("k_top,sample", [(4, 50), (0, 0)])
 def test_2ply_same_seed_same_records(weights_seed0, k_top, sample):
     """Two engines with the same seed, one after the other in one process:

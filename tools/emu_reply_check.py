@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--runs", type=int, default=1)
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--sites", action="store_true", help="EMU_SITES build (-O0 -fno-inline): uniformity only")
+    ap.add_argument("--csrc", default=os.path.join(REPO, "mlp-ppo-2ply-multi_amd", "csrc"),
+                    help="device sources to emulate (e.g. an older tree's csrc, from a git worktree)")
     a = ap.parse_args()
     pos = _fuzz_positions(77, 24) + _random_positions(5, 1500)
     if a.roots:
@@ -47,8 +49,9 @@ def main():
     exe = os.path.join(tmp, "reply_emu")
     opt = ["-O0", "-fno-inline", "-DEMU_SITES"] if a.sites else ["-O1", "-fsanitize=address", "-fno-omit-frame-pointer"]
     cmd = ["g++", "-std=c++20", *opt, "-g", "-w", *["-D" + d for d in a.D],
-           "-I" + os.path.join(REPO, "tests", "cpuwave"), "-I" + os.path.join(REPO, "mlp-ppo-2ply-multi_amd", "csrc"),
-           "-I" + os.path.join(REPO, "include"), "-x", "c++", os.path.join(REPO, "tests", "cpuwave", "reply_emu.cpp"),
+           "-I" + os.path.join(REPO, "tests", "cpuwave"), "-I" + a.csrc,
+           "-I" + os.path.join(a.csrc, "..", "..", "include"), "-x", "c++",
+           os.path.join(REPO, "tests", "cpuwave", "reply_emu.cpp"),
            "-o", exe, "-pthread"]
     subprocess.run(cmd, check=True)
     env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0", "EMU_N_CU": str(a.n_cu)}
@@ -60,9 +63,10 @@ def main():
         t0 = time.time()
         r = subprocess.run([exe, pfile, str(len(pos)), dump], capture_output=True, text=True, env=env)
         print(f"run {run}: rc {r.returncode}, {time.time() - t0:.0f} s, {r.stdout.strip()}", flush=True)
-        if r.returncode != 0:
+        if r.returncode not in (0, 5):   # 5: some job left job_off / job_cnt unwritten (lists still compared)
             print(r.stderr[-3000:])
             sys.exit(1)
+        total_bad += r.returncode == 5
         if a.sites:
             continue
         d = np.fromfile(dump, np.int32)
