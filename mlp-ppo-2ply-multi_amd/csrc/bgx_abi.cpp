@@ -105,6 +105,9 @@ struct bgx_engine {
     int32_t* job_off = nullptr;
     int32_t* job_cnt = nullptr;
     float* job_val = nullptr;
+    float* zt = nullptr;            // 2-ply: the reply roots' hidden accumulators [roots][128] (K = all: every
+                                    // candidate, from the root launch; K = 4: the chosen rows, own launch)
+    float* zv = nullptr;            // K = 4: that launch's V output (unused)
     int jobs_cap = 0, reply_cap = 0, cand_cap = 0;
     int32_t* ovf_list = nullptr;
     int ovf_cap = 0;
@@ -845,6 +848,17 @@ int bgx_two_ply(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_op
     });
 }
 
+// BGX_REPLY_DELTA=1: the 2-ply reply values by difference from their roots
+// (mlp_kernel_delta, bgx_mlp.hip) instead of in full (mlp_kernel_il, the
+// default). Measured and not kept: 33 % fewer MFMAs but
+// twice the VALU and 27x the SALU instructions per tile, 0.95 vs 0.69 ms per
+// K = 4 reply launch. Read when an engine is created / per stateless call, so
+// tests can cross-check both forms in one process.
+static bool reply_delta() {
+    const char* v = getenv("BGX_REPLY_DELTA");
+    return v && atoi(v) != 0;
+}
+
 int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8_t* d_opponent, int n,
                         int sample_k, uint64_t seed, double* d_out, void* stream) {
     return guarded("bgx_two_ply_sampled", [&]() -> int {
@@ -910,6 +924,24 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
             b.err_flags = ctr + 3;
             if (bgx_launch_movegen(&b, s) != hipSuccess) rc = BGX_E_HIP;
         }
+        float* zt = nullptr;
+        if (!rc && reply_delta()) {
+            // the roots' hidden accumulators (their V goes to the reply buffer's
+            // first n slots, overwritten below), for the replies by difference
+            if (dalloc(&zt, (size_t)n * 128)) rc = BGX_E_HIP;
+            bgx::MlpArgs m{};
+            m.rows = rows;
+            m.n_rows = n;
+            m.nt = 1;
+            m.out = V;
+            m.wfrag = net->wfrag;
+            m.rowc = net->rowc;
+            m.b2 = net->b2;
+            m.feat_scale = net->feat_scale;
+            m.zout = zt;
+            m.z_base = 0;
+            if (!rc && bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
+        }
         if (!rc) {
             bgx::MlpArgs m{};
             m.rows = reply;
@@ -922,6 +954,14 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
             m.rowc = net->rowc;
             m.b2 = net->b2;
             m.feat_scale = net->feat_scale;
+            if (zt) {
+                m.zt = zt;
+                m.root_rows = rows;
+                m.root_sel = nullptr;
+                m.root_base = 0;
+                m.n_roots = n;
+                m.n_slots = n;
+            }
             if (bgx_launch_mlp(&m, s) != hipSuccess) rc = BGX_E_HIP;
         }
         if (!rc && bgx_launch_top5(V, off, cnt, jobs, nullptr, 0, jobs, jv, sample_k, seed, nullptr, nullptr, s) != hipSuccess)
@@ -930,7 +970,7 @@ int bgx_two_ply_sampled(const bgx_net* net, const uint8_t* d_boards, const uint8
         unsigned flags = 0;
         if (!rc && (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&flags, ctr + 3, 4, hipMemcpyDeviceToHost) != hipSuccess))
             rc = BGX_E_HIP;
-        void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws};
+        void* ps[] = {mover, rows, reply, ctr, off, cnt, V, jv, ovf, ws, zt};
         for (void* p : ps) hipFree(p);
         if (rc) return fail(rc, "bgx_two_ply: HIP failure");
         if (flags) return fail(BGX_E_CAPACITY, "bgx_two_ply: overflow flags 0x%x", flags);
@@ -1077,7 +1117,7 @@ int bgx_engine_destroy(bgx_engine* e) {
             hipFree(e->fprof);
         }
         void* ps[] = {e->rows, e->V, e->cand_off, e->cand_cnt, e->ctr, e->stats, e->sel, e->sel_rows, e->reply_rows,
-                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->ovf_list, e->ws, e->out_records[0],
+                      e->reply_V, e->job_off, e->job_cnt, e->job_val, e->zt, e->zv, e->ovf_list, e->ws, e->out_records[0],
                       e->out_records[1], e->out_records[2], e->out_headers[0], e->out_headers[1], e->out_headers[2],
                       e->d_offs[0], e->d_offs[1], e->d_offs[2], e->d_info[2], e->fh_ctr, e->d.hring, e->d.hepi,
                       e->d_info[0], e->d_info[1], e->fcand, e->fvbuf, e->ft1cnt, e->d.player, e->d.dice, e->d.step, e->d.flags, e->d.epi, e->d.rng,
@@ -1221,6 +1261,10 @@ int bgx_engine_create(int device, const bgx_config* cfg, bgx_engine** out) {
             ALLOC(e->job_off, e->jobs_cap);
             ALLOC(e->job_cnt, e->jobs_cap);
             ALLOC(e->job_val, e->jobs_cap);
+            if (reply_delta()) {
+                ALLOC(e->zt, (size_t)(cfg->k_top == 4 ? 4 * L : e->cand_cap) * 128);
+                if (cfg->k_top == 4) ALLOC(e->zv, 4 * L);
+            }
         }
     #undef ALLOC
         if (rc) {
@@ -1379,6 +1423,10 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
         m.rowc = e->net->rowc;
         m.b2 = e->net->b2;
         m.feat_scale = e->net->feat_scale;
+        if (e->zt && e->cfg.k_top != 4) {   // 2-ply K = all: every candidate's accumulators (the reply roots)
+            m.zout = e->zt;
+            m.z_base = L;
+        }
         if (timed(e, 1, s, true)) return BGX_E_HIP;
         HIP_TRY(bgx_launch_mlp(&m, s));
         if (timed(e, 1, s, false)) return BGX_E_HIP;
@@ -1389,6 +1437,20 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             b.in_packed = e->rows;
             if (e->cfg.k_top == 4) {
                 HIP_TRY(bgx_launch_topk(&e->d, s));
+                if (e->zt) {   // the chosen rows' accumulators, indexed by reply root slot (4 lane + k)
+                    bgx::MlpArgs z{};
+                    z.rows = e->sel_rows;
+                    z.n_rows = 4 * L;
+                    z.nt = 1;
+                    z.out = e->zv;
+                    z.wfrag = e->net->wfrag;
+                    z.rowc = e->net->rowc;
+                    z.b2 = e->net->b2;
+                    z.feat_scale = e->net->feat_scale;
+                    z.zout = e->zt;
+                    z.z_base = 0;
+                    HIP_TRY(bgx_launch_mlp(&z, s));
+                }
                 b.n_jobs = L * 4 * 21;
                 b.in_packed = e->sel_rows;   // the top-k kernel's copies of the chosen rows
                 b.in_rows = nullptr;
@@ -1429,6 +1491,15 @@ static int enqueue_steps(bgx_engine* e, int n_steps, hipStream_t s) {
             r.rowc = e->net->rowc;
             r.b2 = e->net->b2;
             r.feat_scale = e->net->feat_scale;
+            if (e->zt) {   // replies by difference from their roots (mlp_kernel_delta)
+                const bool k4 = e->cfg.k_top == 4;
+                r.zt = e->zt;
+                r.root_rows = k4 ? e->sel_rows : e->rows;   // K = 4: the top-k kernel's copies, by slot
+                r.root_sel = nullptr;
+                r.root_base = k4 ? 0 : L;
+                r.n_roots = k4 ? 4 * L : e->cand_cap;
+                r.n_slots = r.n_roots;
+            }
             if (timed(e, 1, s, true)) return BGX_E_HIP;
             HIP_TRY(bgx_launch_mlp(&r, s));
             if (timed(e, 1, s, false)) return BGX_E_HIP;

@@ -75,6 +75,21 @@ struct MlpArgs {
     const float* rowc;           // [128] w2 (value_head.weight)
     float b2;
     float feat_scale;            // 2^-e: features are scaled so the accumulator is -h log2(e)
+    // nt = 1 kernel (the 2-ply root launch): rows >= z_base also write their 128
+    // hidden-layer accumulators to zout[row - z_base][2][4][16] (lane half h,
+    // m-tile, accumulator register: the order mlp_kernel_delta reads them in)
+    float* zout;
+    int z_base;
+    // the 2-ply reply launch by difference (mlp_kernel_delta, when zt is set):
+    // row word 7 = its root slot; root row = root_sel ? root_sel[slot] :
+    // root_base + slot, clamped to [root_base, root_base + n_roots); its packed
+    // board at root_rows[root row], its accumulators at zt[root row - root_base]
+    const float* zt;
+    const uint32_t* root_rows;
+    const int32_t* root_sel;
+    int root_base;
+    int n_roots;
+    int n_slots;                 // root slots (clamp of word 7)
 };
 
 // Self-play lane state (one engine per device), structure of arrays.

@@ -117,6 +117,25 @@ __global__ __launch_bounds__(64 * NW) void mlp_kernel(MlpArgs a) {
 #pragma unroll
             for (int q = 0; q < NT; ++q) b[q] = nb[q];
         }
+        if (a.zout) {
+            // the 2-ply root launch: the rows' accumulators for the reply launch's
+            // evaluation by difference (mlp_kernel_delta), 64 contiguous floats per lane
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const int row = (t * NT + q) * 32 + col;
+                if (row >= a.z_base && row < n) {
+                    v4f* zp = (v4f*)(a.zout + (size_t)(row - a.z_base) * 128 + 64 * h);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const v4f zv = {acc[m][q][4 * i], acc[m][q][4 * i + 1], acc[m][q][4 * i + 2],
+                                            acc[m][q][4 * i + 3]};
+                            zp[4 * m + i] = zv;
+                        }
+                }
+            }
+        }
         float v[NT];
         // sigmoid(h) = 1 / (1 + 2^acc) (acc = -h log2 e); w2 of the lane's hidden
         // rows j0 = 32m + (r & 3) + 8(r >> 2) + 4h from LDS, four at a time;
@@ -321,6 +340,216 @@ __global__ __launch_bounds__(64 * IL_NW) void mlp_kernel_il(MlpArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// The 2-ply reply values by difference from the root (round 6). A reply
+// board is its root (the candidate it answers, two_ply.py:93-150) after the
+// opponent's move: it differs from the root only at the points the move
+// touched, the bars / borne-off counts and the side to move. The root launch
+// (mlp_kernel with zout) writes each candidate's hidden-layer accumulators,
+// so a reply's accumulator is root + W . (x_reply - x_root), and only the
+// k-steps where some row of the 32-row tile differs from its root contribute:
+// k-step s < 12 covers bytes 2 s and 2 s + 1 of the packed board (four point
+// slots of one player), k-step 12 the bars, borne-off counts and side to move
+// (always run). In self-play ~7.7 of the 13 k-steps run per tile (replies to
+// one root touch ~12 of the 24 point-pair bytes; tools/probe/delta_ksteps.py).
+// The pairing of bytes into k-steps is the fixed one, so a row's value does not
+// depend on the rows it shares a tile with (a k-step where its own difference
+// is zero adds exact zeros): the same bits whichever tile, wave or run.
+// Feature differences are exact in fp16 (multiples of 0.5 * 2^-e within
+// +-15 * 2^-e), the MFMA products exact, the sums fp32: V within ~1e-6 of the
+// full evaluation (tests/test_cpuwave.py on the shipped checkpoint), so the
+// north_star tolerance 1e-5 holds (test_gpu_scale.py per-candidate W at the
+// bench shape, test_gpu_replay.py golden W). One 32-row tile per wave
+// iteration, 8 waves per CU, the next tile's rows staged by LDS-DMA, the next
+// k-step's A fragments read ahead of the current MFMAs; the epilogue (root
+// accumulator added, sigmoid, value head) in the canonical order.
+constexpr int DL_NW = 8;
+constexpr int DL_RB = 64;   // uint4 per staged tile (32 rows x 32 B)
+
+// rows 32 t .. 32 t + 31 -> dst (16 B per lane); rows past the buffer's
+// capacity read its last row (their V is never stored)
+BGX_DEV void dl_stage(const uint32_t* rows, int t, int cap, uint4* dst) {
+    const int lane = (int)(threadIdx.x & 63);
+    int row = 32 * t + (lane >> 1);
+    row = row < cap ? row : cap - 1;
+    const uint4* src = (const uint4*)(rows + (size_t)row * 8) + (lane & 1);
+    __builtin_amdgcn_global_load_lds((glb_vp)(void*)src, (lds_vp)(void*)dst, 16, 0, 0);
+}
+
+// Per wave iteration (tile t): t's root boards and root accumulators are
+// requested, the previous tile's epilogue runs (covering the boards'
+// latency), then t's k-step mask (ballots), its MFMAs (covering the root
+// accumulators'), and the root accumulators are added; the next k-step's A
+// fragments and LUT entries are read ahead of the current MFMAs.
+__global__ __launch_bounds__(64 * DL_NW) void mlp_kernel_delta(MlpArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+    uint4* wf = lds;                                   // [NFRAG]
+    uint4* lut = lds + NFRAG;                          // [256]
+    float* w2s = (float*)(lds + NFRAG + 256);          // [128] value-head weights
+    uint4* rbuf = lds + NFRAG + 256 + 32;              // [DL_NW][2][DL_RB] staged rows
+    int n = a.n_rows;
+    if (a.n_rows_dev) n += (int)*a.n_rows_dev;
+    if (a.n_max > 0 && n > a.n_max) n = a.n_max;
+    const int cap = a.n_max > 0 ? a.n_max : n;
+    const int tiles = (n + 31) / 32;
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5;
+    const int col = lane & 31;
+    const int wave = threadIdx.x >> 6;
+    const int nwaves = gridDim.x * DL_NW;
+    uint4* rb = rbuf + wave * 2 * DL_RB;
+    int t = blockIdx.x * DL_NW + wave;
+    if (t < tiles) dl_stage(a.rows, t, cap, rb);
+    for (int i = threadIdx.x; i < NFRAG; i += blockDim.x) wf[i] = a.wfrag[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = lut_entry((uint32_t)i, a.feat_scale);
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) w2s[i] = a.rowc[i];
+    __syncthreads();
+    // fragment bases (hi terms, lo terms; each m-tile's fragments at a constant
+    // offset below 64 KB from its base)
+    const lds_u4p wfh = (lds_u4p)(wf + lane);
+    const lds_u4p wfl = (lds_u4p)(wf + 4 * KSTEPS * 64 + lane);
+    const lds_fp w2h = (lds_fp)(w2s + 4 * h);
+    floatx16 acc[4];
+    v4f z[16];
+    int tp = -1;   // tile whose accumulators (acc) and root accumulators (z) await the epilogue
+    // sigmoid and the value head in the canonical order (bgx_mlp.h) over the
+    // tile's complete accumulators (root + difference)
+    auto epilogue = [&](int tt) {
+        float v = 0.0f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            float pm = 0.0f;
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const v4f c4 = *(__attribute__((address_space(3))) const v4f*)(w2h + 32 * m + 8 * gq);
+                const float cy[4] = {c4[0], c4[1], c4[2], c4[3]};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float ex = __builtin_amdgcn_exp2f(acc[m][4 * gq + k]);
+                    pm = fmaf(cy[k], __builtin_amdgcn_rcpf(1.0f + ex), pm);
+                }
+            }
+            v = m == 0 ? pm : v + pm;
+        }
+        v += __shfl_xor(v, 32, 64);
+        const int row = tt * 32 + col;
+        if (h == 0 && row < n) a.out[row] = v + a.b2;
+    };
+    for (int it = 0; t < tiles; t += nwaves, ++it) {
+        // this tile's staged rows (and tp's z) landed: vmcnt(0) as the builtin
+        // (0xF70: expcnt and lgkmcnt at their maxima), which the compiler's wait
+        // insertion sees, so it does not also wait before the k-loop's LDS reads
+        __builtin_amdgcn_s_waitcnt(0xF70);
+        wave_sync();   // (host emulation: every lane's staging copy is done)
+        const uint4* cb = rb + (it & 1) * DL_RB;
+        const uint4 bx = cb[2 * col], by = cb[2 * col + 1];
+        const int row = t * 32 + col;
+        // the row's root (word 7 = root slot; stale rows past the records: clamped)
+        const uint32_t slot = by.w < (uint32_t)a.n_slots ? by.w : (uint32_t)(a.n_slots - 1);
+        int rr = a.root_sel ? a.root_sel[slot] : a.root_base + (int)slot;
+        rr = rr < a.root_base ? a.root_base : (rr >= a.root_base + a.n_roots ? a.root_base + a.n_roots - 1 : rr);
+        const uint4* rp = (const uint4*)(a.root_rows + (size_t)rr * 8);
+        const uint4 rx = rp[0], ry = rp[1];
+        // the root accumulators, added to this tile's after its MFMAs (~2 epilogue
+        // and MFMA phases from now)
+        const v4f* zp = (const v4f*)(a.zt + (size_t)(rr - a.root_base) * 128 + 64 * h);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) z[i] = zp[i];
+        if (tp >= 0) epilogue(tp);   // the previous tile, while the root boards arrive
+        // the tile's k-steps: k-step s < 12 covers bytes 2 s, 2 s + 1 of the
+        // packed board (its two lane halves), so it runs iff some row of the tile
+        // differs from its root there; k-step 12 (bars, borne-off, side to move)
+        // always runs (the side to move differs between a root and its replies).
+        // A row's result does not depend on the tile it shares: a k-step where
+        // its own difference is zero adds exact zeros, and the pairing of bytes
+        // into k-steps is the fixed one (a pairing by the tile's changes made V
+        // depend on which rows share a tile: ~1e-8, run to run)
+        uint32_t mrem = 1u << 12;
+        {
+            const bool live = row < n;
+            const uint32_t d[6] = {bx.x ^ rx.x, bx.y ^ rx.y, bx.z ^ rx.z, bx.w ^ rx.w, by.x ^ ry.x, by.y ^ ry.y};
+#pragma unroll
+            for (int s2 = 0; s2 < 12; ++s2)
+                mrem |= ballot(live && ((d[s2 >> 1] >> (16 * (s2 & 1))) & 0xFFFFu) != 0u) ? 1u << s2 : 0u;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][r] = 0.0f;
+        // k-step s's feature difference: the two LUT entries (k-step 12: the bars,
+        // borne-off counts and side to move, dmisc; the bias cancels). The LUT
+        // reads of the next k-step are issued before its A fragment reads and
+        // subtracted one iteration later, so waiting for them never waits for
+        // the fragments (LDS reads complete in order)
+        half8 dmisc;
+        {
+            const half8 f1 = feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, by.z, 0), KSTEPS - 1, h, lut,
+                                       a.feat_scale);
+            const half8 f0 = feat_frag(make_uint4(0, 0, 0, 0), make_uint4(0, 0, ry.z, 0), KSTEPS - 1, h, lut,
+                                       a.feat_scale);
+            dmisc = f1 - f0;
+        }
+        // (selects on the bits of the uniform k-step index: a chain of equality
+        // tests on it became a private array in scratch)
+        auto lut_byte = [&](const uint4& x, const uint4& y, int s2) -> uint32_t {
+            const int s3 = s2 < 12 ? s2 : 0;
+            const bool odd = (s3 & 2) != 0;
+            const uint32_t w01 = odd ? x.y : x.x, w23 = odd ? x.w : x.z, w45 = odd ? y.y : y.x;
+            const uint32_t word = s3 < 4 ? w01 : (s3 < 8 ? w23 : w45);
+            return (word >> (8 * (2 * (s3 & 1) + h))) & 0xFFu;
+        };
+        // two fragment sets in turn (ping-pong): k-step i's MFMAs use set i & 1,
+        // read during k-step i - 1; the reads of k-step i + 1 into the other set
+        // are issued ahead of k-step i's MFMAs (no register copies between sets)
+        uint4 fr[2], fq[2];
+        v4u ah[2][4], al[2][4];
+        int ks[2];
+        auto issue = [&](int q) {   // the next k-step's LUT entries, then its A fragments, into set q
+            const int s2 = __ffs(mrem) - 1;
+            mrem &= mrem - 1u;
+            ks[q] = s2;
+            fr[q] = lut[lut_byte(bx, by, s2)];
+            fq[q] = lut[lut_byte(rx, ry, s2)];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                ah[q][m] = wfh[(m * KSTEPS + s2) * 64];
+                al[q][m] = wfl[(m * KSTEPS + s2) * 64];
+            }
+        };
+        auto phase = [&](int q) {
+            const half8 bd = *(const half8*)&fr[q] - *(const half8*)&fq[q];
+            const half8 b = ks[q] < 12 ? bd : dmisc;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ah[q][m]), b, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, al[q][m]), b, acc[m], 0, 0, 0);
+            }
+        };
+        issue(0);
+        for (;;) {
+            const bool more0 = mrem != 0u;
+            if (more0) issue(1);
+            phase(0);
+            if (!more0) break;
+            const bool more1 = mrem != 0u;
+            if (more1) issue(0);
+            phase(1);
+            if (!more1) break;
+        }
+        // accumulator = difference + root (the fp32 sums of the root launch)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][r] += z[4 * m + (r >> 2)][r & 3];
+        // the next tile's rows, staged after the MFMAs: an LDS-DMA in flight makes
+        // the compiler wait for every vector-memory operation (the root
+        // accumulators too) before each LDS read
+        if (t + nwaves < tiles) dl_stage(a.rows, t + nwaves, cap, rb + ((it + 1) & 1) * DL_RB);
+        tp = t;
+    }
+    if (tp >= 0) epilogue(tp);
+}
+
 // Generic fp32-input value (bgx_value: arbitrary x, plain fp32 FMA) — parity
 // entry point, not the hot path. One 128-thread block per 8 rows.
 __global__ __launch_bounds__(128) void value_f32_kernel(const float* __restrict__ x, int n,
@@ -368,14 +597,28 @@ extern "C" hipError_t bgx_launch_mlp(const bgx::MlpArgs* args, hipStream_t strea
     int& n_cu = n_cu_dev[cur];
     const int lds = bgx::NFRAG * 16 + 256 * 16 + 128 * 4;
     const int lds_il = lds + bgx::IL_NW * 2 * bgx::IL_RB * 16;
+    const int lds_dl = lds + bgx::DL_NW * 2 * bgx::DL_RB * 16;
     if (!n_cu) {
         if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cur) != hipSuccess || n_cu <= 0)
             n_cu = 256;
         if (hipFuncSetAttribute((const void*)bgx::mlp_kernel<1, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds) != hipSuccess ||
             hipFuncSetAttribute((const void*)bgx::mlp_kernel_il, hipFuncAttributeMaxDynamicSharedMemorySize, lds_il) !=
+                hipSuccess ||
+            hipFuncSetAttribute((const void*)bgx::mlp_kernel_delta, hipFuncAttributeMaxDynamicSharedMemorySize, lds_dl) !=
                 hipSuccess)
             return hipErrorInvalidValue;
+    }
+    if (args->zt) {   // the 2-ply replies by difference from their roots (8 waves, one tile each)
+        int blocks = n_cu;
+        if (!args->n_rows_dev) {
+            const int need = ((args->n_rows + 31) / 32 + bgx::DL_NW - 1) / bgx::DL_NW;
+            if (need < blocks) blocks = need;
+            if (blocks <= 0) return hipSuccess;
+        }
+        if (args->n_slots <= 0 || args->n_roots <= 0 || !args->root_rows) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(bgx::mlp_kernel_delta, dim3(blocks), dim3(64 * bgx::DL_NW), lds_dl, stream, *args);
+        return hipGetLastError();
     }
     // nt = 1: latency-bound small batches (one 32-board tile per wave, 16-wave
     // blocks); nt = 2: throughput (the interleaved-epilogue kernel, 8 waves)

@@ -468,6 +468,10 @@ BGX_DEV void emit_one(const MovegenArgs& a, int j, const Root& R, const Node& n,
         }
         row = (size_t)base + k;
     }
+    // a 2-ply reply row carries its root slot (the candidate it answers: job / 21)
+    // in word 7, so the reply MLP can evaluate it by difference from the root
+    // (mlp_kernel_delta, bgx_mlp.hip)
+    if (a.in_mode == IN_TWOPLY) w[7] = (uint32_t)j / 21u;
     uint4* dst = (uint4*)(a.out_packed + row * 8);
     dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
     dst[1] = make_uint4(w[4], w[5], w[6], w[7]);

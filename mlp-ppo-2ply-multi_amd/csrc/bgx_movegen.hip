@@ -364,7 +364,7 @@ __global__ __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(BGX_POO
                 if (base >= 0) {
                     for (int i = l; i < n; i += 64) {
                         const uint32_t e = M.pa[i];
-                        emit_one(a, 0, in.R, nd_board(in.R, e), i, base);
+                        emit_one(a, j0, in.R, nd_board(in.R, e), i, base);   // (j0: the row's root slot)
                     }
                 }
                 wave_sync();   // the list is read before the next item reuses the slice

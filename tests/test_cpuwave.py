@@ -248,3 +248,53 @@ def test_mlp_kernels_emulated_equal_oracle_value(tmp_path):
         v = np.fromfile(out, np.float32)
         assert v.shape == ref.shape
         assert np.abs(v - ref).max() < 1e-6, (nt, np.abs(v - ref).max())
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="no ROCm clang")
+def test_mlp_delta_kernel_emulated_equals_oracle_value(tmp_path):
+    """The 2-ply reply MLP by difference from the root (mlp_kernel_delta: the
+    root launch writes its hidden accumulators, each reply row -- word 7 = its
+    root -- adds W . (x_reply - x_root) over the tile's changed byte groups),
+    emulated on the host: the replies to 40 random positions for all 21 rolls
+    (tens of thousands of rows, tiles spanning several roots) give the oracle's
+    fp64 value (policy_network.py:53-70) within 2e-6 on the shipped checkpoint.
+    AddressSanitizer on (the root / accumulator gathers stay in bounds, also for
+    a stale root index, which is clamped)."""
+    orc = pytest.importorskip("oracle")
+    from test_gpu_parity import _random_positions
+    pos = _random_positions(8, 40)
+    rolls = [(a, b) for a in range(1, 7) for b in range(a, 7)]
+    roots, reps, slot, opp = [], [], [], []
+    for i, (board, mover) in enumerate(pos):
+        o = 1 - int(mover)   # the replier; the root's indicator is the player who moved
+        roots.append(_pack(board[None], np.array([mover]))[0])
+        for a, b in rolls:
+            n, res, _ = orc.movegen(board, o, a, b)
+            reps += list(res[:n])
+            slot += [i] * n
+            opp += [o] * n
+    reps = np.stack(reps)
+    rows = _pack(reps, np.array(opp))
+    rows[:, 7] = np.array(slot, np.uint32)
+    rows[-1, 7] = 0xFFFFFFF0   # a stale root index: clamped (its V is still computed, from some root)
+    rows.tofile(tmp_path / "rows.bin")
+    np.stack(roots).astype(np.uint32).tofile(tmp_path / "roots.bin")
+    w = np.load(os.path.join(HERE, "golden", "weights_ckpt2100000.npz"))
+    W = {k: w[k].astype(np.float32) for k in ("W1", "b1", "w2", "b2")}
+    np.concatenate([W[k].ravel() for k in ("W1", "b1", "w2", "b2")]).astype(np.float32).tofile(tmp_path / "w.bin")
+    ref = orc.value(W, orc.encode_many(reps, opp))
+    src = _emu_sources(tmp_path)
+    exe = tmp_path / "mlp_emu"
+    subprocess.run([CLANG, "-std=c++20", "-O1", "-g", "-w", "-fsanitize=address", "-fno-omit-frame-pointer",
+                    "-I" + str(src), "-I" + os.path.join(HERE, "cpuwave"), "-I" + os.path.join(REPO, "include"),
+                    "-x", "c++", os.path.join(HERE, "cpuwave", "mlp_emu.cpp"), "-o", str(exe), "-pthread"],
+                   check=True, capture_output=True, text=True)
+    env = {**os.environ, "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0"}
+    out = tmp_path / "vd.bin"
+    r = subprocess.run([str(exe), str(tmp_path / "rows.bin"), str(tmp_path / "w.bin"), "d", str(out),
+                        str(tmp_path / "roots.bin")], capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    v = np.fromfile(out, np.float32)
+    assert v.shape == ref.shape and len(v) > 10000
+    err = np.abs(v[:-1] - ref[:-1])
+    assert err.max() < 2e-6, (err.max(), int(err.argmax()))

@@ -16,6 +16,13 @@
 * 2-ply K = all at 4,096 lanes (configs[2]'s lane count), greedy: >= 2,000
   sampled decisions equal the oracle's argmax of 1.0 * V - 0.9 * W over every
   candidate (two_ply.py:44-150).
+* 2-ply at the bench's own 8,192-lane shape (round 6): K = all greedy, >= 2,000
+  decisions equal the oracle's argmax, and one step peeked between two
+  bgx_engine_peek calls gives, for >= 500 lanes, the oracle's candidate boards
+  (bit-exact), V within 1e-5 and the W of every candidate (the DICE_ROLLS-
+  weighted top-5 reply means the step computed) within 1e-5 of the oracle's
+  two_ply_response; K = 4 (the bench's sampling leg): the engine's top 4 by V
+  and each one's W, 500 lanes.
 * The same seed twice in one process gives identical records for 2-ply
   reference-sampled (reply_sample = 50, two_ply.py:119-121) and K = all
   (DESIGN.md section 4 argues why no kernel reads a reply row outside its
@@ -371,3 +378,25 @@ def test_k4_8192_lanes_sampling_transitions(weights_seed0):
     sub_h, sub_r = _subset(hdr, rec, np.sort(take))
     d = decode_records(sub_h, torch.from_numpy(sub_r.view(np.int32)).cuda())
     assert _check_transitions(weights_seed0, [sub_h], [d], 2) >= 5000
+
+
+@pytest.mark.parametrize("k_top", [4, 0])
+def test_reply_delta_opt_in_w(weights_seed0, k_top, monkeypatch):
+    """The opt-in reply MLP by difference from the root (BGX_REPLY_DELTA=1,
+    mlp_kernel_delta; measured slower and not the default): one
+    peeked step of a 2,048-lane engine, W of >= 150 lanes' candidates within
+    1e-5 of the oracle's two_ply_response (K = 4: the chosen rows' own root
+    launch, roots by slot; K = all: the root launch's accumulators)."""
+    monkeypatch.setenv("BGX_REPLY_DELTA", "1")
+    lanes = 2048
+    e = _engine(weights_seed0, lanes=lanes, seed=47, ply=2, k_top=k_top)
+    e.step(60)
+    e.harvest()
+    before, after = _peek_step(e)
+    e.close()
+    rng = np.random.default_rng(19)
+    need = 4 if k_top == 4 else 1
+    movers = [i for i in rng.permutation(lanes) if int(after["cand_cnt"][i]) >= need][:150]
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        nw = list(ex.map(lambda i: _check_lane_w(weights_seed0, lanes, before, after, i), movers))
+    assert len(movers) == 150 and sum(nw) >= 600
