@@ -209,8 +209,23 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
     # lanes start together from the reset; `desync` untimed steps
     # (harvested, and gathered at N > 1, like the timed ones) spread them over
     # their games so the timed window holds finished episodes, refills and
-    # harvests, then the driver's warmup
+    # harvests, then the driver's warmup. The desync lasts at least
+    # --desync-ms of GPU time too (more chunks of --harvest-every steps): 300
+    # 1-ply steps are ~11 ms, after which the driver's 20-step window still ran
+    # ~4 % slower than after ~45 ms (220-225 vs 232-233 M env steps/s,
+    # tools/runs/r6_desync.sh; the GPU idles during the CPU baseline before it)
+    t_ds = time.perf_counter()
     run(desync)
+    desync_run = desync
+    while True:   # the same number of extra chunks on every rank (the gathers count batches)
+        eng.sync()
+        more = (time.perf_counter() - t_ds) * 1e3 < args.desync_ms
+        if world > 1:
+            more = max_over_ranks(1.0 if more else 0.0, world) > 0
+        if not more:
+            break
+        run(harvest_every)
+        desync_run += harvest_every
     run(warmup)
     eng.sync()
     s0 = eng.stats()
@@ -242,6 +257,7 @@ def run_engine(args, world, rank, ply, k_top, lanes, steps, warmup, harvest_ever
         import torch.distributed as dist
         dist.barrier()
         hg.close()
+    d["desync_steps_run"] = desync_run
     return el, d, tm, d_tm, gathered, harvested
 
 
@@ -454,6 +470,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--desync-steps", type=int, default=300,
                     help="untimed steps before the warmup so lanes are spread over their games (SURVEY 8d)")
+    ap.add_argument("--desync-ms", type=float, default=50.0,
+                    help="... and at least this much GPU time (more chunks of --harvest-every steps), so the "
+                         "window does not start on a GPU that idled through the CPU baseline")
     ap.add_argument("--harvest-every", type=int, default=300,
                     help="steps per bgx_step launch between harvests (<= ring - max_steps)")
     ap.add_argument("--two-ply-steps", type=int, default=100, help="2-ply K=4 leg (configs[4]); 0 = skip")
@@ -530,7 +549,7 @@ def main():
                 # 2-ply: reply rows the movegen reserved but left unwritten (the MLP
                 # evaluates them; the algorithmic figures below leave them out)
                 "gap_rows_frac": sum_over_ranks(d_["gap_rows"], world) / max(1, sum_over_ranks(d_["value_rows"], world)),
-                "roofline": roof_, "kernels": kern_, "desync_steps": desync,
+                "roofline": roof_, "kernels": kern_, "desync_steps": int(d_.get("desync_steps_run", desync)),
                 "seed": args.seed if seed is None else seed}
         if world > 1:
             out_["gathered_episodes"], out_["gathered_records"] = gathered_
