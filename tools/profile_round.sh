@@ -17,11 +17,11 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --outpu
 echo "[3/4] PMC traffic passes"
 for leg in 1ply_fused 2ply_k4 2ply_kall; do
   if [ $leg = 1ply_fused ]; then
-    ARGS="--steps 600 --warmup 300 --timing-steps 300 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"; RX="fused_step"
+    ARGS="--steps 600 --warmup 300 --timing-steps 300 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --config2-steps 0 --no-cpu-baseline"; RX="fused_step"
   elif [ $leg = 2ply_k4 ]; then
-    ARGS="--ply 2 --steps 60 --warmup 20 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"; RX="movegen|mlp_kernel"
+    ARGS="--ply 2 --steps 60 --warmup 20 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --config2-steps 0 --no-cpu-baseline"; RX="movegen|mlp_kernel"
   else
-    ARGS="--ply 2 --k-top 0 --steps 10 --warmup 2 --desync-steps 60 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --no-cpu-baseline"; RX="movegen|mlp_kernel"
+    ARGS="--ply 2 --k-top 0 --steps 10 --warmup 2 --desync-steps 60 --timing-steps 1 --two-ply-steps 0 --kall-steps 0 --config1-steps 0 --config2-steps 0 --no-cpu-baseline"; RX="movegen|mlp_kernel"
   fi
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "[pmc] $leg $c"
