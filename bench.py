@@ -342,22 +342,28 @@ def cpu_baseline(procs, seconds_1ply, seeds, seconds_2ply):
     return out
 
 
-def _pmc(leg, group, key):
+def _pmc(leg, group, key, lanes=8192):
     """A per-launch PMC figure from the committed round profile
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py from separate
-    rocprofv3 --pmc passes of this same bench workload), with its source."""
+    rocprofv3 --pmc passes of this same bench workload), with its source.
+    The profile's legs run at 8,192 lanes; a leg at another lane count reads
+    its own l<lanes>_ entry or nothing (never the 8,192-lane figure)."""
     prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if lanes != 8192:
+        leg = f"l{lanes}_{leg}"
     try:
         with open(prof) as f:
             j = json.load(f)
         v = j.get(leg, {}).get(group, {}).get(key)
-        src = f"profiles/pmc_traffic.json ({j.get('round', '?')}: {j.get('workload', '?')})"
+        if v is None:
+            return None, None
+        src = f"profiles/pmc_traffic.json [{leg}] ({j.get('round', '?')}: {j.get('workload', '?')})"
         return v, src
     except (OSError, ValueError):
         return None, None
 
 
-def roofline_fused(d, tm):
+def roofline_fused(d, tm, lanes=8192):
     """The fused 1-ply step kernel (one launch = all steps of a step() call):
     the whole path's algorithmic bytes (54 B per movegen job +
     901 B per evaluated board) and MLP FLOPs over its average launch.
@@ -391,22 +397,22 @@ def roofline_fused(d, tm):
     r["kernel"] = "bgx::fused_step_kernel (movegen + encode + MLP + select + env step, all steps of a launch)"
     r["achieved_basis"] = "SURVEY 8d algorithmic bytes (54 B per movegen job + 901 B per evaluated board)"
     # PMC bytes per step of the same workload x the steps of this bench's launches
-    per_step, src = _pmc("1ply_fused", "fused", "hbm_bytes_per_step")
+    per_step, src = _pmc("1ply_fused", "fused", "hbm_bytes_per_step", lanes)
     r["traffic"] = per_step * k["steps_per_launch"] if per_step else None
     r["traffic_source"] = src if per_step else None
     r["physical_gbs"] = r["traffic"] / (launch * 1e-3) / 1e9 if r["traffic"] else None
     r["physical_frac"] = r["physical_gbs"] / HBM_PEAK_GBS if r["physical_gbs"] else None
     for key in ("valu_busy", "mfma_busy", "lds_busy", "salu_busy", "wait_frac", "issue_stall_frac", "waves_per_cu"):
-        r[key] = _pmc("1ply_fused", "fused", key)[0]
+        r[key] = _pmc("1ply_fused", "fused", key, lanes)[0]
     r["mfma_frac_algorithmic"] = m["frac"]
     return r, {"fused_step": k, "fused_step_mfma": m}
 
 
-def roofline_for(d, tm, leg):
+def roofline_for(d, tm, leg, lanes=8192):
     """Dominant kernel's algorithmic rate over its average launch (HIP events),
     from the timed pass `d` (stats deltas) / `tm` (event totals)."""
     if tm["mlp_launches"] == 0 and tm["movegen_launches"] > 0:
-        return roofline_fused(d, tm)
+        return roofline_fused(d, tm, lanes)
     el = d["elapsed_s"]
     mg_ms, mlp_ms = tm["movegen_ms"], tm["mlp_ms"]
     out = {}
@@ -431,11 +437,12 @@ def roofline_for(d, tm, leg):
     r["kernel"] = (("movegen launch = bgx::movegen_few_kernel + bgx::movegen_block_kernel" if leg == "1ply" else
                     "movegen launches = (few | pool) + bgx::movegen_block_kernel")
                    if dom == "movegen" else "bgx::mlp_kernel")
-    r["traffic"], r["traffic_source"] = _pmc(leg, dom, "hbm_bytes_per_launch") if leg != "1ply" else (None, None)
+    r["traffic"], r["traffic_source"] = (_pmc(leg, dom, "hbm_bytes_per_launch", lanes) if leg != "1ply"
+                                         else (None, None))
     if r["traffic"]:
         r["physical_gbs"] = r["traffic"] / (out[dom]["avg_launch_ms"] * 1e-3) / 1e9
     for key in ("valu_busy", "mfma_busy", "wait_frac", "issue_stall_frac", "waves_per_cu"):
-        v, _src = _pmc(leg, dom, key) if leg != "1ply" else (None, None)
+        v, _src = _pmc(leg, dom, key, lanes) if leg != "1ply" else (None, None)
         if v is not None:
             r[key] = v
     return r, out
@@ -538,7 +545,7 @@ def main():
                                                    timing_steps=timing_steps, desync=desync, seed=seed)
         el_ = max_over_ranks(el_, world)
         per_rank = [int(x) for x in all_ranks(d_["env_steps"], world)]
-        roof_, kern_ = roofline_for(dtm_, tm_, name) if timing_steps > 0 else (None, None)
+        roof_, kern_ = roofline_for(dtm_, tm_, name, lanes) if timing_steps > 0 else (None, None)
         out_ = {"value": sum(per_rank) / el_, "unit": "env_steps/s", "steps": steps, "lanes_per_gpu": lanes,
                 "ms_per_step": el_ / steps * 1e3, "env_steps_per_rank": per_rank,
                 "decisions_per_s": sum_over_ranks(d_["decisions"], world) / el_,

@@ -36,14 +36,17 @@ def group(name):
 
 def main(out):
     res = {"round": os.path.basename(os.path.normpath(out)),
-           "workload": "bench.py defaults: 8,192 lanes per GPU, seeded xavier weights, T=1.5",
+           "workload": "bench.py defaults: 8,192 lanes per GPU (l<n>_ legs: n lanes), seeded xavier weights, T=1.5",
            "source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
                      "fused 1-ply leg (--kernel-include-regex fused_step, 300 steps per dispatch) and 2-ply K=4 leg "
                      "(--kernel-include-regex 'movegen|mlp_kernel', 60 steps); SQ busy ratios from "
                      "tools/sq_counters.sh (sq_<leg>.json)",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts 1/2 of wide "
                          "coalesced reads; narrow movegen reads are uncalibrated, the raw value is kept beside it)"}
-    for leg in ("1ply_fused", "2ply_k4", "2ply_kall"):
+    # legs at another lane count (tools/profile_round.sh <dir> <lanes>) are l<lanes>_<leg>
+    pre = sorted({os.path.basename(d).split("_")[1] + "_" for d in glob.glob(os.path.join(out, "pmc_l*_*"))
+                  if os.path.isdir(d)})
+    for leg in [p + b for p in [""] + pre for b in ("1ply_fused", "2ply_k4", "2ply_kall")]:
         f = per_kernel(os.path.join(out, f"pmc_{leg}_FETCH_SIZE"))
         w = per_kernel(os.path.join(out, f"pmc_{leg}_WRITE_SIZE"))
         if not f and not w:
@@ -76,7 +79,7 @@ def main(out):
                 legd[g]["steps_per_launch"] = FUSED_STEPS_PER_DISPATCH
                 legd[g]["hbm_bytes_per_step"] = legd[g]["hbm_bytes_per_launch"] / FUSED_STEPS_PER_DISPATCH
         # SQ counter ratios of the same leg's kernels (tools/sq_summary.py)
-        sq_leg = {"1ply_fused": "1ply", "2ply_k4": "2ply_k4", "2ply_kall": "2ply_kall"}[leg]
+        sq_leg = leg[:-len("_fused")] if leg.endswith("1ply_fused") else leg
         try:
             sq = json.load(open(os.path.join(out, f"sq_{sq_leg}.json")))["kernels"]
             for g in ("movegen", "mlp", "fused"):
@@ -92,6 +95,8 @@ def main(out):
                         legd[g]["sq_kernel"] = k
         except (OSError, ValueError, KeyError):
             pass
+        if leg.startswith("l"):
+            legd["lanes"] = int(leg[1:leg.index("_")])
         res[leg] = legd
     print(json.dumps(res, indent=1))
 
