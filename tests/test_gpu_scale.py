@@ -22,7 +22,8 @@
   (bit-exact), V within 1e-5 and the W of every candidate (the DICE_ROLLS-
   weighted top-5 reply means the step computed) within 1e-5 of the oracle's
   two_ply_response; K = 4 (the bench's sampling leg): the engine's top 4 by V
-  and each one's W, 500 lanes.
+  and each one's W, 500 lanes. The same peeked check at configs[2]'s 4,096
+  lanes for both legs bench.py times there (K = 4 and K = all).
 * The same seed twice in one process gives identical records for 2-ply
   reference-sampled (reply_sample = 50, two_ply.py:119-121) and K = all
   (DESIGN.md section 4 argues why no kernel reads a reply row outside its
@@ -305,6 +306,27 @@ def test_k4_8192_lanes_w(weights_seed0):
     with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
         nw = list(ex.map(lambda i: _check_lane_w(weights_seed0, lanes, before, after, i), movers))
     assert len(movers) == 500 and sum(nw) == 2000
+
+
+@pytest.mark.parametrize("k_top", [4, 0])
+def test_configs2_4096_lanes_w(weights_seed0, k_top):
+    """configs[2]'s own shape (4,096 lanes, bench.py's configs2_4096_lanes
+    legs; a grid of half the 8,192-lane one per launch): one peeked step, the
+    candidates, V and every scored candidate's W against the oracle (K = 4:
+    300 lanes with >= 4 moves, sampling; K = all: 250 lanes, greedy)."""
+    lanes = 4096
+    e = _engine(weights_seed0, lanes=lanes, seed=53 + k_top, ply=2, k_top=k_top, greedy=k_top == 0)
+    e.step(100)
+    e.harvest()
+    before, after = _peek_step(e)
+    e.close()
+    rng = np.random.default_rng(23)
+    need, n_lanes = (4, 300) if k_top == 4 else (1, 250)
+    movers = [i for i in rng.permutation(lanes) if int(after["cand_cnt"][i]) >= need][:n_lanes]
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        nw = list(ex.map(lambda i: _check_lane_w(weights_seed0, lanes, before, after, i), movers))
+    assert len(movers) == n_lanes
+    assert sum(nw) == 4 * n_lanes if k_top == 4 else sum(nw) >= 2000, sum(nw)
 
 
 @pytest.mark.parametrize("k_top,sample", [(4, 50), (0, 0)])
