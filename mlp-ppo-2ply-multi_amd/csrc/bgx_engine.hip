@@ -220,6 +220,10 @@ BGX_DEV bool small_double(int j) {   // DICE_ROLLS index 0 = 1-1, 6 = 2-2, 11 = 
 #ifndef BGX_T5_GL
 #define BGX_T5_GL 4   // lanes per job (A/B builds: 2, 4, 8)
 #endif
+#ifndef BGX_T5_VB
+#define BGX_T5_VB 0   // > 0: 16-byte block loads, this many per lane per batch (A/B; 0: 8 scalar loads)
+#endif
+typedef float t5v4 __attribute__((ext_vector_type(4)));
 constexpr int T5_GL = BGX_T5_GL;
 constexpr int T5_B = 8;    // loads in flight per lane
 __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
@@ -269,7 +273,47 @@ __global__ __launch_bounds__(256) void top5_kernel(const float* __restrict__ V,
         u32x4 pk = {0u, 0u, 0u, 0u};
         if (samp) pk = philox(skey, 0x2B1A000000000000ull ^ salt, (uint64_t)j);
         float t[5] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#if BGX_T5_VB
+        // 16-byte blocks: the job's 4 lanes read 64 contiguous bytes per load
+        // (one or two cache lines instead of the 8 scalar loads' 8 line
+        // accesses per job), blocks aligned on the address: a0 <= o is the
+        // first element whose address is 16-byte aligned, so a block may start
+        // up to 3 elements before the job and end up to 3 after it; those
+        // elements are masked by their index (they belong to other jobs or gap
+        // rows, and reading them is in bounds: dalloc pads every buffer by 16 B
+        // and a0 >= -3 stays at or after the aligned allocation start)
+        // Sampled jobs (rare: 1-1 / 2-2 / 3-3 past sample_k replies) take the
+        // scalar loop below: with the permutation's cycle walk inside this
+        // loop's unrolled elements, hipcc 7.2 gave wrong, run-dependent top-5s
+        // on the GPU (the host emulation of the same source was right).
+        const int mis = (int)(((uintptr_t)V >> 2) & 3u);
+        const int a0 = ((o + mis) & ~3) - mis, end = samp ? o : o + c;
+        for (int b0 = a0 + 4 * gl; b0 < end; b0 += 4 * T5_GL * BGX_T5_VB) {
+            t5v4 xb[BGX_T5_VB];
+#pragma unroll
+            for (int u = 0; u < BGX_T5_VB; ++u) {
+                const int i0 = b0 + 4 * T5_GL * u;
+                xb[u] = i0 < end ? *(const t5v4*)(V + i0) : t5v4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            }
+#pragma unroll
+            for (int u = 0; u < BGX_T5_VB; ++u) {
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int i = b0 + 4 * T5_GL * u + q4;
+                    float v = i >= o && i < end ? xb[u][q4] : -INFINITY;
+#pragma unroll
+                    for (int i5 = 0; i5 < 5; ++i5) {
+                        const float hi = fmaxf(t[i5], v);
+                        v = fminf(t[i5], v);
+                        t[i5] = hi;
+                    }
+                }
+            }
+        }
+        for (int k0 = gl; samp && k0 < c; k0 += T5_B * T5_GL) {
+#else
         for (int k0 = gl; k0 < c; k0 += T5_B * T5_GL) {
+#endif
             float xv[T5_B];
 #pragma unroll
             for (int u = 0; u < T5_B; ++u) {
